@@ -1,0 +1,100 @@
+/*
+ * dsb_host.h — host-side (C) part of the MI355X deSAMBA classify library.
+ *
+ * The host owns everything the reference does outside classify_seq: index files,
+ * FASTQ/FASTA parsing with the reference's kseq + kt_pipeline batch semantics,
+ * SAM formatting, the taxonomy and meta_analysis.  The classify path itself runs in
+ * HIP kernels behind dsb_gpu.h.
+ */
+#ifndef DSB_HOST_H
+#define DSB_HOST_H
+#include <stdint.h>
+#include <stddef.h>
+#include <pthread.h>
+#include "dsb_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ index */
+typedef struct {
+	uint32_t p_tid;
+	char rank[20];
+	char name[201];
+} dsb_taxon_t; /* TAXONOMY_rank (idx.h:11-15) */
+
+typedef struct dsb_index {
+	/* host copies (big tables are released after the device upload unless kept) */
+	uint8_t *bwt_occ; uint64_t byteLen;
+	uint64_t rank[6];
+	uint64_t *hash_index;
+	dsb_sa_t *sa; uint64_t sa_size;
+	uint64_t dollor_pos;
+	uint8_t *ek0, *ek1; uint64_t ek_size, ek_mask; int l_ek, single_base_max;
+	dsb_unitig_t *uni; uint64_t n_uni;
+	uint8_t *ref_bin; uint64_t ref_bin_n, ref_bin_padded;
+	uint64_t n_ref;
+	char (*ref_name)[128];
+	uint64_t *ref_seq_l, *ref_seq_offset;
+	uint64_t *r_p; uint64_t n_rp;
+	int *Q_MEM;               /* DSB_Q_MEM_PAD */
+	int Q_LV[DSB_LV_DIM * DSB_LV_DIM];
+	int filter_min_length, filter_min_score, filter_min_score_LV3;
+	/* taxonomy (cly_mt.c:590-670) */
+	dsb_taxon_t *tax; uint64_t max_tid;
+	/* device side (dsb_gpu.c) */
+	void *gpu;
+	/* per-thread_id state (cly_mt.c:1279-1307) */
+	pthread_mutex_t state_mutex;
+	struct dsb_thread_state *states;
+} dsb_index;
+
+/* Load deSAMBA.{bwt,sa,exk0,exk1,exki,unv,ref_b,ref_i,ref_p} (idx.c:1103-1160, bwt.c:68-104).
+ * Returns 0 on success; on failure writes a message to err. */
+int dsb_index_load_files(dsb_index *ix, const char *dir, char *err, size_t errn);
+/* MAPQ tables (cly_mt.c:396-420), P_E 0.15, L_REF = 4 * ref_bin.n */
+void dsb_mapq_tables(dsb_index *ix, double P_E, uint64_t L_REF);
+/* Taxonomy (cly_mt.c:590-670). Returns 0 on success. */
+int dsb_taxonomy_load(dsb_index *ix, const char *dir, char *err, size_t errn);
+void dsb_index_free_host_tables(dsb_index *ix);
+/* Fill a dsb_dindex_t with the host pointers (CPU emulation / tests only) */
+void dsb_index_host_view(const dsb_index *ix, dsb_dindex_t *d);
+
+/* ------------------------------------------------------------------ reads */
+typedef struct {
+	uint64_t name_off, seq_off, qual_off; /* offsets into the batch text arena */
+	uint32_t seq_l;                       /* kseq seq.l */
+	int32_t qual_null;                    /* qual.s was NULL: printf prints "(null)" */
+} dsb_rec_t;
+
+typedef struct {
+	char *arena; uint64_t arena_n, arena_m;
+	dsb_rec_t *rec; uint64_t n, m;
+} dsb_reads_t;
+
+/* Parse `len` bytes of FASTQ/FASTA text with the semantics of read_reads + kseq_read +
+ * kt_pipeline (cly_mt.c:29-43,361-381; utils.c:841-977; kthread.c:114-197). */
+int dsb_parse_reads(const char *buf, uint64_t len, dsb_reads_t *out);
+/* read a whole (optionally gzip) file or memory buffer (gzip auto-detected) */
+int dsb_slurp_path(const char *path, char **buf, uint64_t *len);
+int dsb_inflate_if_gzip(const char *in, uint64_t in_n, char **buf, uint64_t *len, int *owned);
+void dsb_reads_free(dsb_reads_t *r);
+
+/* ------------------------------------------------------------------ output */
+typedef struct { char *s; uint64_t l, m; } dsb_str;
+void dsb_str_put(dsb_str *s, const char *p, uint64_t n);
+void dsb_str_printf(dsb_str *s, const char *fmt, ...);
+
+enum { DSB_OUT_SAM = 1, DSB_OUT_SAM_FULL = 2, DSB_OUT_DES = 3, DSB_OUT_DES_FULL = 4 };
+void dsb_format_read(dsb_str *out, const dsb_index *ix, const dsb_reads_t *r, uint64_t i,
+		     const dsb_read_out_t *ro, const dsb_hit_out_t *hits, int format, int max_sec_N);
+
+/* ------------------------------------------------------------------ meta analysis */
+int dsb_meta_analysis(dsb_index *ix, const char *input, uint64_t input_n, char **output, uint64_t *output_n,
+		      int flag, uint64_t max_snapshot_len, char **human_snapshot, uint64_t *human_snapshot_n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

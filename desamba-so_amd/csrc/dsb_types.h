@@ -1,0 +1,85 @@
+/*
+ * dsb_types.h — plain-old-data types shared by the C host code and the HIP kernels.
+ *
+ * Everything on the classify path is integer arithmetic; widths mirror the reference
+ * exactly because the reference relies on uint32 wrap-around in several places
+ * (SURVEY Appendix A, H11).  Reference citations are to /root/reference/src.
+ */
+#ifndef DSB_TYPES_H
+#define DSB_TYPES_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* SA sample, one per 8 BWT rows (bwt.h:6-13) */
+typedef struct { uint32_t unitig_ID, offset; } dsb_sa_t;
+/* UNITIG (idx.h:28-32); the loader appends a sentinel (idx.c:1127) */
+typedef struct { uint32_t ref_list, length; } dsb_unitig_t;
+
+/* REF_POS (idx.h:42-48): u64 bitfield {global_offset:40, ref_ID:23, direction:1} */
+#define DSB_RP_OFF(x) ((x) & 0xFFFFFFFFFFull)
+#define DSB_RP_REF(x) ((uint32_t)(((x) >> 40) & 0x7FFFFF))
+
+/* Constants of the classify path (src/idx.h, src/cly.c) */
+#define DSB_L_PRE_IDX 13
+#define DSB_PRE_IDX_MASK 0x3FFFFFFull
+#define DSB_Q_MEM_MAX 2000
+#define DSB_Q_MEM_PAD 4096  /* device copy padded; see DESIGN.md "unpinned corners" */
+#define DSB_LV_DIM 20
+#define DSB_MIN_UNI_L 35
+#define DSB_MIN_READ_LEN 40
+
+/*
+ * Device-visible index: raw pointers into HBM (or host memory for the
+ * kernel-logic CPU emulation used only by tests).
+ */
+typedef struct {
+	const uint8_t *bwt_occ;      /* 168-B blocks per 256 BWT symbols (bwt.c:32-42) */
+	uint64_t byteLen;
+	uint64_t rank[6];            /* rank[5] = rank[0]-1 (bwt.c:81) */
+	const uint64_t *hash_index;  /* (2^26+1) u64, 13-mer prefix -> SA interval (bwt.c:83-85) */
+	const dsb_sa_t *sa;
+	uint64_t sa_size;
+	uint64_t dollor_pos;         /* unitig_v.n - 2 (idx.c:1128) */
+	const uint8_t *ek0, *ek1;    /* e-kmer Bloom tables (idx.c:1108-1121) */
+	uint64_t ek_size, ek_mask;
+	int l_ek, single_base_max;   /* set_ekmer_par (idx.c:966-982) */
+	const dsb_unitig_t *uni;     /* n_uni + 1 entries (sentinel) */
+	uint64_t n_uni;
+	const uint8_t *ref_bin;      /* 2-bit MSB-first packed reference, zero padded */
+	uint64_t ref_bin_n;          /* bytes in the file (padding not counted) */
+	uint64_t ref_bin_padded;     /* bytes readable */
+	const uint64_t *ref_seq_offset, *ref_seq_l; /* REF_INFO (idx.h:22-26) minus the name */
+	uint64_t n_ref;
+	const uint64_t *r_p;         /* REF_POS raw */
+	uint64_t n_rp;
+	const int *Q_MEM;            /* DSB_Q_MEM_PAD ints */
+	const int *Q_LV;             /* [20][20] row-major: Q_LV[ed*20 + len] */
+	int filter_min_length, filter_min_score, filter_min_score_LV3;
+} dsb_dindex_t;
+
+/* Output record per hit (what output_one_result_sam needs, cly_mt.c:229-327) */
+typedef struct {
+	uint32_t ref_ID;
+	uint32_t sum_score;
+	uint32_t t_st, t_ed, q_st, q_ed;
+	uint32_t indel;
+	uint8_t direction, primary, pri_index, pad;
+} dsb_hit_out_t;
+
+/* Per-read result summary */
+typedef struct {
+	uint32_t n_hit;        /* hits written to the read's output slot */
+	uint32_t n_anchor;     /* anchor_v.n at the end (DES output) */
+	uint32_t fast;         /* results->fast_classify */
+	uint32_t status;       /* 0 ok; bit0 overflow (re-run with larger workspace) */
+	uint32_t reached_update; /* read reached the max_read_l update (cly.c:2953) */
+	uint32_t pad[3];
+} dsb_read_out_t;
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1620 @@
+/*
+ * dsb_classify.h — the per-read classify path (reference classify_seq, src/cly.c:3059-3127)
+ * restated for one GPU lane per read, over a per-read workspace carved from HBM.
+ *
+ * Pointers of the reference (chain_anchor_pre, chain_anchor_cur, SEARCH_DIR members) are
+ * indices here; dynamic vectors (kvec) are fixed-capacity arrays whose overflow marks the
+ * read for a second pass with a larger workspace (never a CPU fallback).
+ */
+#ifndef DSB_CLASSIFY_H
+#define DSB_CLASSIFY_H
+#include "dsb_core.h"
+
+/* ------------------------------------------------------------------ per-read types */
+typedef struct { uint32_t offset, len; uint8_t top, p0, p1, p2; } dsb_seed_t; /* CLY_seed, cly.h:27-32 */
+
+typedef struct { /* Anchor, cly.h:44-61 (pointers -> indices) */
+	uint64_t global_offset;
+	uint32_t ref_ID, ref_offset, index_in_read;
+	int32_t pre;            /* chain_anchor_pre, -1 = NULL */
+	uint16_t mtch_len;      /* Anchor_map (cly.h:34-42) */
+	int16_t score;
+	uint8_t left_len, left_ED, rigt_len, rigt_ED;
+	uint16_t seed_ID, chain_id;
+	uint8_t direction, anchor_useless, duplicate, pad;
+} dsb_anchor_t;
+
+typedef struct { /* chain_item, cly.h:69-89 */
+	uint32_t ref_ID;
+	int32_t q_t_dis;
+	uint32_t sum_score, anchor_number;
+	uint8_t direction, with_top_anchor, primary, pri_index;
+	uint32_t t_st, t_ed, q_st, q_ed, indel, chain_id;
+	int32_t cur;            /* chain_anchor_cur */
+} dsb_chain_t;
+
+typedef struct { uint32_t t_pos, q_pos, len, score; } dsb_spd_t; /* spd_match, cly.h:127-133 */
+
+typedef struct { /* MEM_rst, src/cly.c:614-622 */
+	int match_len;
+	uint64_t sp, sa_sp;
+	int sa_sp_l, kmer_index, read_offset;
+} dsb_mem_t;
+
+#define DSB_WIN_MID 64
+#define DSB_WIN_RL (64 + 2064 + 64)
+#define DSB_WIN_BYTES (DSB_WIN_RL + 1064 + 64)
+typedef struct { uint16_t next; uint16_t seed_ID_s_or_e; } dsb_sch_t; /* seed_con_hash, cly.h:120-125 */
+
+typedef struct { /* SEARCH_DIR, src/cly.c:941-949 */
+	uint32_t seed_off;      /* index of seed_v_f in the seed buffer */
+	uint32_t l_seed_v_f;
+	uint32_t strand;        /* 0: forward buffer half, 1: reverse half */
+	uint32_t direction;
+	uint32_t total_score;
+} dsb_sdir_t;
+
+/* workspace capacities (elements) */
+typedef struct {
+	uint32_t anc, hit, sms;
+} dsb_caps_t;
+
+/* Per-read workspace (all pointers into the read's arena) */
+typedef struct {
+	const dsb_dindex_t *ix;
+	uint32_t L;             /* read length */
+	uint8_t *bin;           /* F at bin[0..L), R at bin[L..2L); guard before/after */
+	const uint64_t *exF, *exR; /* exist bits per k-mer position (K_seed output) */
+	dsb_seed_t *seeds;      /* (L>>1)+20 (+spill) entries; R seeds at L>>2 (src/cly.c:1238,1252) */
+	dsb_anchor_t *anc; uint32_t n_anc;
+	dsb_anchor_t *anc_tmp;
+	uint32_t *sidx, *stmp;  /* msort permutation scratch (max(anc, hit) entries) */
+	dsb_chain_t *hit; uint32_t n_hit;
+	dsb_chain_t *hit_tmp;
+	dsb_spd_t *sms; uint32_t n_sms;
+	uint32_t *hh[2], *ht[2], *hn[2], *hk[2]; /* read 9-mer hash: heads, tails, next, kmer */
+	dsb_sch_t *sch;         /* 256 + 2*400 */
+	uint8_t *win;           /* DSB_WIN_BYTES: sdp_middle ref[2000] and sdp_right/left ref[1000] windows */
+	dsb_mem_t *mem;         /* 256 MEM results (slow mode) */
+	uint64_t *spset;        /* 500 */
+	dsb_caps_t cap;
+	uint32_t overflow;
+	uint32_t fast_classify;
+	dsb_sdir_t sd[2];
+	int max_read_l;         /* Classify_buff_pool.max_read_l, supplied (H2) */
+	uint32_t reached_update;
+	/* optional counters for algorithmic-byte accounting (bench) */
+	uint64_t *stats;
+} dsb_read_ws;
+
+enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, DSB_ST_REFPOS,
+       DSB_ST_GETREF_B, DSB_ST_ANCHOR, DSB_ST_CHAIN, DSB_ST_EK1, DSB_ST_EK2, DSB_ST_N };
+
+DSB_HD int dsb_exist_bit(const uint64_t *ex, uint32_t k)
+{
+	return (int)((ex[k >> 6] >> (k & 63)) & 1);
+}
+
+/* ------------------------------------------------------------------ seeding */
+/* search_exist_kmer_M2, src/cly.c:1066-1155, on precomputed exist bits */
+DSB_HD uint32_t dsb_search_exist(const uint64_t *ex, uint32_t l_kmer_v, dsb_seed_t *seed_v, uint32_t direction)
+{
+	uint32_t l_seed_v = 0;
+	const uint32_t STEP_EK = 3;
+	if (direction == DSB_FORWARD) {
+		for (uint32_t i = STEP_EK - 1; i < l_kmer_v; i += STEP_EK) {
+			if (dsb_exist_bit(ex, i)) {
+				uint32_t offset = i, len = 1;
+				for (int j = 1; j < (int)STEP_EK; ++j) {
+					if (dsb_exist_bit(ex, i - j)) { offset--; len++; }
+					else break;
+				}
+				for (int j = 1; i + j < l_kmer_v; ++j) {
+					if (dsb_exist_bit(ex, i + j)) {
+						len++;
+						if (len > 60) break; /* the i += 50 is overwritten below */
+					} else break;
+				}
+				seed_v[l_seed_v].offset = offset;
+				seed_v[l_seed_v].len = len;
+				l_seed_v++;
+				i = offset + len;
+			}
+		}
+	} else {
+		for (int i = (int)l_kmer_v - (int)STEP_EK; i >= 0; i -= STEP_EK) {
+			if (dsb_exist_bit(ex, (uint32_t)i)) {
+				uint32_t offset = i, len = 1;
+				for (int j = 1; j < (int)STEP_EK; ++j) {
+					if (dsb_exist_bit(ex, (uint32_t)(i + j))) { offset++; len++; }
+					else break;
+				}
+				for (int j = 1; j <= i; ++j) {
+					if (dsb_exist_bit(ex, (uint32_t)(i - j))) {
+						len++;
+						if (len > 60) break;
+					} else break;
+				}
+				seed_v[l_seed_v].offset = offset - len + 1;
+				seed_v[l_seed_v].len = len;
+				l_seed_v++;
+				i = (int)(offset - len);
+			}
+		}
+	}
+	return l_seed_v;
+}
+
+/* get_seed_vector_M2, src/cly.c:1157-1229 */
+DSB_HD void dsb_seed_vector(dsb_read_ws *w, uint32_t strand, uint32_t seed_off, uint32_t direction, dsb_sdir_t *sd)
+{
+	uint32_t l_kmer_buff = w->L - w->ix->l_ek + 1;
+	dsb_seed_t *seed_v = w->seeds + seed_off;
+	uint32_t l_seed_v = dsb_search_exist(strand ? w->exR : w->exF, l_kmer_buff, seed_v, direction);
+	uint32_t total_score = 0;
+	int max_index = 0;
+	uint32_t max_length = 0, index_end = 100; /* SEED_RANGE */
+	for (uint32_t m = 0; m < l_seed_v; m++) {
+		seed_v[m].top = 0;
+		uint32_t key = (direction == DSB_FORWARD) ? seed_v[m].offset
+						       : l_kmer_buff - seed_v[m].offset - seed_v[m].len;
+		if (key < index_end) {
+			if (max_length < seed_v[m].len) {
+				max_length = seed_v[m].len;
+				max_index = m;
+			}
+			seed_v[max_index].top = 0;
+		} else {
+			seed_v[max_index].top = 1;
+			index_end += 100;
+			total_score += max_length;
+			max_index = m;
+			max_length = seed_v[m].len;
+		}
+	}
+	seed_v[max_index].top = 1; /* also when l_seed_v == 0 (writes a stale slot, as the reference) */
+	total_score += max_length;
+	sd->seed_off = seed_off;
+	sd->l_seed_v_f = l_seed_v;
+	sd->strand = strand;
+	sd->direction = direction;
+	sd->total_score = total_score;
+}
+
+/* getIsland, src/cly.c:1231-1263: forward seeds at seed_v[0..), reverse at seed_v[L>>2..) */
+DSB_HD void dsb_get_island(dsb_read_ws *w)
+{
+	dsb_seed_vector(w, 0, 0, DSB_FORWARD, &w->sd[0]);
+	dsb_seed_vector(w, 1, w->L >> 2, DSB_REVERSE, &w->sd[1]);
+	if (w->sd[0].total_score < w->sd[1].total_score) {
+		dsb_sdir_t t = w->sd[0];
+		w->sd[0] = w->sd[1];
+		w->sd[1] = t;
+	}
+}
+
+/* ------------------------------------------------------------------ FM search */
+typedef struct { uint64_t *set; int l, m; } dsb_spset_t;
+
+/* sp_set_insert, src/cly.c:1281-1293 */
+DSB_HD int dsb_spset_insert(uint64_t node, dsb_spset_t *s)
+{
+	if (s->l == s->m)
+		s->l = 0;
+	int i = 0;
+	for (; i < s->l; i++)
+		if (s->set[i] == node)
+			return 0;
+	s->set[i] = node;
+	s->l++;
+	return 1;
+}
+
+/* bwt_single_search, src/cly.c:1339-1378; `string` indexes the read buffer, read backwards */
+DSB_HD void dsb_single_search(dsb_read_ws *w, uint64_t sp, const uint8_t *string, int max_match_len,
+			       dsb_spset_t *sp_set, dsb_mem_t *mem_rst)
+{
+	const dsb_dindex_t *ix = w->ix;
+	uint64_t new_sp, sa_sp = ~0ull;
+	int match_len = 0, sa_sp_l = 0;
+	while (1) {
+		if (match_len >= max_match_len)
+			break;
+		if ((sp & 7) == 0) {
+			sa_sp = sp;
+			sa_sp_l = 0;
+		} else
+			sa_sp_l--;
+		uint8_t c;
+		new_sp = dsb_lf(ix, sp, &c);
+		if (w->stats) w->stats[DSB_ST_OCC]++;
+		if (c != *string)
+			break;
+		match_len++;
+		string--;
+		if (dsb_spset_insert(new_sp, sp_set) == 0) {
+			mem_rst->match_len = -1000;
+			return;
+		}
+		sp = new_sp;
+	}
+	mem_rst->sp = sp;
+	mem_rst->match_len = match_len;
+	mem_rst->sa_sp = sa_sp;
+	mem_rst->sa_sp_l = sa_sp_l;
+}
+
+/* bwt_MEM_search, src/cly.c:1383-1442 */
+DSB_HD int dsb_mem_search(dsb_read_ws *w, const uint8_t *string, uint64_t pre_v, int max_rst, int l_min_mth,
+			   int l_max_mth, dsb_spset_t *sp_set, dsb_mem_t *mem_rst)
+{
+	const dsb_dindex_t *ix = w->ix;
+	int n_rst = 0;
+	uint64_t sp = ix->hash_index[pre_v], ep = ix->hash_index[pre_v + 1], new_sp, new_ep;
+	if (w->stats) w->stats[DSB_ST_MEMSEARCH]++;
+	string -= DSB_L_PRE_IDX;
+	int match_len = DSB_L_PRE_IDX;
+	uint8_t c;
+	while (1) {
+		c = *string;
+		string--;
+		uint8_t c2 = c;
+		new_sp = ix->rank[c] + dsb_occ(ix, sp, &c);
+		new_ep = ix->rank[c2] + dsb_occ(ix, ep, &c2);
+		if (w->stats) w->stats[DSB_ST_OCC] += 2;
+		if (match_len >= l_min_mth - 1) {
+			if (new_sp + max_rst >= new_ep)
+				break;
+			if (match_len >= l_max_mth)
+				return 0;
+		}
+		if (new_sp + 1 >= new_ep)
+			break;
+		match_len++;
+		sp = new_sp;
+		ep = new_ep;
+	}
+	if (new_sp >= new_ep)
+		return 0;
+	if (new_sp + 1 == new_ep) {
+		if (dsb_spset_insert(new_sp, sp_set) == 0)
+			return 0;
+		dsb_single_search(w, new_sp, string, DSB_MAX(0, l_max_mth - match_len), sp_set, mem_rst + n_rst);
+		mem_rst[n_rst].match_len += match_len + 1;
+		if (mem_rst[n_rst].match_len >= l_min_mth)
+			n_rst++;
+	} else {
+		for (uint64_t c_sp = new_sp; c_sp < new_ep; c_sp++) {
+			if (dsb_spset_insert(c_sp, sp_set) == 0)
+				continue;
+			dsb_single_search(w, c_sp, string, DSB_MAX(0, l_max_mth - match_len), sp_set, mem_rst + n_rst);
+			mem_rst[n_rst].match_len += match_len + 1;
+			if (mem_rst[n_rst].match_len >= l_min_mth)
+				n_rst++;
+		}
+	}
+	return n_rst;
+}
+
+/* ------------------------------------------------------------------ seed mapping */
+/* get_uni, src/cly.c:466-491 (the `uni_offset < 0` loop never runs: uint32) */
+DSB_HD uint32_t dsb_get_uni(const dsb_dindex_t *ix, uint64_t bwt_pos, int search_l, uint64_t *global_offset,
+			     uint32_t *uni_offset_)
+{
+	dsb_sa_t s = ix->sa[bwt_pos >> 3];
+	uint32_t u = s.unitig_ID;
+	uint32_t uni_offset = s.offset + search_l + 1;
+	if (search_l > 0)
+		for (; uni_offset >= ix->uni[u].length && u < ix->n_uni;) { /* sentinel stops the walk */
+			uni_offset -= (ix->uni[u].length + 1);
+			u++;
+		}
+	uint64_t rp = ix->r_p[ix->uni[u].ref_list];
+	*global_offset = DSB_RP_OFF(rp) + uni_offset;
+	*uni_offset_ = uni_offset;
+	return u;
+}
+
+/* get_new_ed, src/cly.c:624-689 */
+DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t *len_, uint32_t *l_mem_ext,
+			    int32_t q_off, uint64_t t_off, uint32_t l_read, int is_FWD)
+{
+	uint8_t qbuf[32], tbuf[32];
+	for (int k = 0; k < 32; k++) { qbuf[k] = DSB_STACK_PATTERN; tbuf[k] = DSB_STACK_PATTERN; }
+	uint8_t *q = qbuf + 8, *t = tbuf + 8;
+	uint32_t len, max_len;
+	if (is_FWD) {
+		if (q_off < 0)
+			q_off = 0;
+		max_len = q_off;
+		len = DSB_MIN(12u, max_len);
+		for (uint8_t k = 0; k < len; k++)
+			q[k] = q_b[q_off - k];
+	} else {
+		max_len = l_read - q_off;
+		len = DSB_MIN(12u, max_len);
+		q = q_b + q_off;
+	}
+	dsb_get_ref(w->ix, t, t_off, len, !is_FWD);
+	if (len > 0 && t[0] == q[0]) {
+		int mtc;
+		do {
+			for (mtc = 0; mtc < (int)len; mtc++)
+				if (t[mtc] != q[mtc])
+					break;
+			if (mtc > 0) {
+				*l_mem_ext += mtc;
+				max_len -= mtc;
+				len = DSB_MIN(12u, max_len);
+				if (is_FWD) {
+					q_off -= mtc;
+					t_off -= mtc;
+					for (uint8_t k = 0; k < len; k++)
+						q[k] = q_b[q_off - k];
+				} else {
+					t_off += mtc;
+					q += mtc;
+				}
+				dsb_get_ref(w->ix, t, t_off, len, !is_FWD);
+			}
+		} while (mtc > 0);
+	}
+	*e_d = dsb_lv_extd(t, len, q, len);
+	*len_ = len;
+}
+
+typedef struct { uint8_t *bin_read; uint32_t read_L; uint16_t seed_ID; uint32_t direction; } dsb_seedinfo_t;
+
+/* Q_MEM[l]: the reference reads past its 2000 entries for exact matches >= 2000 bp
+ * (unpinned); the device table is padded and the index clamped. */
+DSB_HD int dsb_qmem(const dsb_dindex_t *ix, uint32_t l)
+{
+	return ix->Q_MEM[l < DSB_Q_MEM_PAD ? l : DSB_Q_MEM_PAD - 1];
+}
+
+DSB_HD dsb_anchor_t *dsb_push_anchor(dsb_read_ws *w)
+{
+	if (w->n_anc >= w->cap.anc) {
+		w->overflow |= 1;
+		return 0;
+	}
+	return w->anc + w->n_anc++;
+}
+
+#define DSB_LV_L 12
+#define DSB_MIN_S_1 12
+#define DSB_MIN_S_2 20
+/* map_seed, src/cly.c:701-934 */
+DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i)
+{
+	const dsb_dindex_t *ix = w->ix;
+	const int *Q_LV = ix->Q_LV;
+	uint64_t b_p = m_r->sp;
+	int32_t q_off = m_r->read_offset;
+	uint32_t l_m = m_r->match_len;
+	uint8_t *q_b = s_i->bin_read;
+	int32_t uni = -1;
+	uint32_t u_off = 0;
+	uint64_t t_off = 0;
+	uint32_t l_pre = 0, l_suf = 0;
+	uint32_t d_pre = 0, d_suf = 0;
+	int32_t s = 0, max_s = 0;
+	/* stack windows of the reference: q_pre/t_pre/t_suf[LV_L + 1] */
+	uint8_t qpre_b[32], tpre_b[32], tsuf_b[32];
+	for (int k = 0; k < 32; k++) { qpre_b[k] = DSB_STACK_PATTERN; tpre_b[k] = DSB_STACK_PATTERN; tsuf_b[k] = DSB_STACK_PATTERN; }
+	uint8_t *q_pre = qpre_b + 8, *t_pre = tpre_b + 8, *t_suf = tsuf_b + 8;
+	do {
+		uint8_t *q_suf;
+		l_pre = DSB_MIN(q_off + 1, DSB_LV_L);
+		for (uint8_t k = 0; k < l_pre; k++)
+			q_pre[k] = q_b[q_off - k];
+		int s_l = 0;
+		if (m_r->sa_sp != ~0ull) {
+			uni = (int32_t)dsb_get_uni(ix, m_r->sa_sp, m_r->sa_sp_l, &t_off, &u_off);
+			if (w->stats) w->stats[DSB_ST_SA]++;
+		} else {
+			uint8_t c;
+			uint64_t new_sp;
+			while (1) {
+				if ((b_p & 7) == 0)
+					break;
+				new_sp = dsb_lf(ix, b_p, &c);
+				if (w->stats) w->stats[DSB_ST_OCC]++;
+				if (c == 4)
+					break;
+				t_pre[s_l++] = c;
+				b_p = new_sp;
+				if ((uint32_t)s_l >= l_pre)
+					break;
+			}
+			if ((b_p & 7) == 0) {
+				uni = (int32_t)dsb_get_uni(ix, b_p, s_l, &t_off, &u_off);
+				if (w->stats) w->stats[DSB_ST_SA]++;
+			} else
+				l_pre = s_l;
+		}
+		if (uni >= 0) {
+			if (ix->uni[uni].length < DSB_MIN_UNI_L)
+				break;
+			l_pre = DSB_MIN(l_pre, u_off);
+			dsb_get_ref(ix, t_pre, t_off - 1, l_pre, 0);
+		}
+		d_pre = dsb_lv_extd(t_pre, l_pre, q_pre, l_pre);
+		s = dsb_qmem(ix, l_m) + Q_LV[d_pre * DSB_LV_DIM + l_pre];
+		if (s < DSB_MIN_S_1 && l_pre == DSB_LV_L && uni < 0) {
+			s = 0;
+			break;
+		}
+		if (uni < 0) {
+			while (b_p & 7) {
+				uint8_t c;
+				b_p = dsb_lf(ix, b_p, &c);
+				if (w->stats) w->stats[DSB_ST_OCC]++;
+				s_l++;
+			}
+			uni = (int32_t)dsb_get_uni(ix, b_p, s_l, &t_off, &u_off);
+			if (w->stats) w->stats[DSB_ST_SA]++;
+			if (ix->uni[uni].length < DSB_MIN_UNI_L) {
+				s = 0;
+				break;
+			}
+		}
+		int32_t q_off_r = q_off + l_m + 1;
+		uint32_t l_max_suf = DSB_MIN(ix->uni[uni].length - u_off - l_m, s_i->read_L - q_off_r);
+		if (l_max_suf != 0) {
+			l_suf = DSB_MIN(l_max_suf, (uint32_t)DSB_LV_L);
+			q_suf = q_b + q_off_r;
+			dsb_get_ref(ix, t_suf, t_off + l_m, l_suf, 1);
+			if (t_suf[0] == q_suf[0]) {
+				int mtc;
+				do {
+					for (mtc = 0; mtc < (int)l_suf; mtc++)
+						if (t_suf[mtc] != q_suf[mtc])
+							break;
+					if (mtc > 0) {
+						l_m += mtc;
+						s = dsb_qmem(ix, l_m) + Q_LV[d_pre * DSB_LV_DIM + l_pre];
+						l_max_suf -= mtc;
+						l_suf = DSB_MIN(l_max_suf, (uint32_t)DSB_LV_L);
+						q_suf += mtc;
+						dsb_get_ref(ix, t_suf, t_off + l_m, l_suf, 1);
+					}
+				} while (mtc > 0);
+			}
+			d_suf = dsb_lv_extd(t_suf, l_suf, q_suf, l_suf);
+			s += Q_LV[d_suf * DSB_LV_DIM + l_suf];
+		} else
+			l_suf = d_suf = 0;
+		if (s <= DSB_MIN_S_2 && l_suf == DSB_LV_L) {
+			s = 0;
+			break;
+		}
+	} while (0);
+
+	if (s > 0) {
+		/* Anchor_map a_m = {l_m, s, l_pre, d_pre, l_suf, d_suf} (uint16/int16/uint8 fields) */
+		uint16_t am_mtch = (uint16_t)l_m;
+		int16_t am_score = (int16_t)s;
+		uint8_t am_ll = (uint8_t)l_pre, am_le = (uint8_t)d_pre, am_rl = (uint8_t)l_suf, am_re = (uint8_t)d_suf;
+		uint64_t rp_s = ix->uni[uni].ref_list, rp_e = ix->uni[uni + 1].ref_list;
+		int ref_search_l = (l_pre < DSB_LV_L || d_pre == 0);
+		int ref_search_r = (l_suf < DSB_LV_L || d_suf == 0);
+		uint8_t duplicate = 0;
+		if (rp_e - rp_s > 50) {
+			if (!(rp_e - rp_s < 1000))
+				return 50;
+		}
+		for (uint64_t c_r_p = rp_s; c_r_p < rp_e; c_r_p++) {
+			uint64_t rp = ix->r_p[c_r_p];
+			if (w->stats) w->stats[DSB_ST_REFPOS]++;
+			uint32_t ed_l, ed_r, len_l, len_r;
+			uint32_t l_m_ext_l = 0, l_m_ext_r;
+			if (ref_search_l || ref_search_r) {
+				if (ref_search_l) {
+					dsb_get_new_ed(w, q_b, &ed_l, &len_l, &l_m_ext_l, q_off, DSB_RP_OFF(rp) + u_off - 1, s_i->read_L, 1);
+					am_ll = (uint8_t)len_l;
+					am_le = (uint8_t)ed_l;
+				}
+				am_mtch = (uint16_t)(l_m + l_m_ext_l);
+				if (ref_search_r) {
+					l_m_ext_r = 0;
+					dsb_get_new_ed(w, q_b, &ed_r, &len_r, &l_m_ext_r, q_off + l_m + 1, DSB_RP_OFF(rp) + u_off + l_m,
+						       s_i->read_L, 0);
+					am_rl = (uint8_t)len_r;
+					am_re = (uint8_t)ed_r;
+					am_mtch = (uint16_t)(am_mtch + l_m_ext_r);
+				}
+				am_score = (int16_t)(dsb_qmem(ix, am_mtch) + Q_LV[am_le * DSB_LV_DIM + am_ll] +
+						     Q_LV[am_re * DSB_LV_DIM + am_rl]);
+				if (am_score < DSB_MIN_S_2)
+					continue;
+			}
+			max_s = DSB_MAX(max_s, (int32_t)am_score);
+			dsb_anchor_t *a = dsb_push_anchor(w);
+			if (!a)
+				return max_s;
+			if (w->stats) w->stats[DSB_ST_ANCHOR]++;
+			a->direction = (uint8_t)s_i->direction;
+			a->index_in_read = q_off + 1 - l_m_ext_l;
+			a->global_offset = DSB_RP_OFF(rp) + u_off - l_m_ext_l;
+			a->ref_ID = DSB_RP_REF(rp);
+			a->ref_offset = (uint32_t)(a->global_offset - ix->ref_seq_offset[a->ref_ID]);
+			a->mtch_len = am_mtch;
+			a->score = am_score;
+			a->left_len = am_ll; a->left_ED = am_le; a->rigt_len = am_rl; a->rigt_ED = am_re;
+			a->seed_ID = s_i->seed_ID;
+			a->duplicate = duplicate;
+			a->pre = -1;
+			a->chain_id = 0;
+			a->anchor_useless = 0;
+		}
+	}
+	return max_s;
+}
+
+/* ------------------------------------------------------------------ fast / slow */
+#define DSB_MEM_SEARCH_FAST 2
+#define DSB_MIN_MEM_LEN_FAST 21
+/* fast_classify, src/cly.c:1473-1541 */
+DSB_HDN void dsb_fast_classify(dsb_read_ws *w, const dsb_sdir_t *s_d)
+{
+	const dsb_dindex_t *ix = w->ix;
+	uint8_t l_ek = (uint8_t)ix->l_ek;
+	int min_index = DSB_MIN_MEM_LEN_FAST - l_ek;
+	uint8_t *bin_read = w->bin + (s_d->strand ? w->L : 0);
+	dsb_spset_t sp_set = {w->spset, 0, 500};
+	dsb_mem_t m_r[DSB_MEM_SEARCH_FAST];
+	dsb_seed_t *sv_b = w->seeds + s_d->seed_off;
+	uint32_t n_sv = s_d->l_seed_v_f;
+	dsb_seedinfo_t s_i = {bin_read, w->L, 0, s_d->direction};
+	for (uint32_t ci = 0; ci < n_sv; ci++) {
+		dsb_seed_t *c_sv = sv_b + ci;
+		if (c_sv->top == 0)
+			continue;
+		sp_set.l = 0;
+		s_i.seed_ID = (uint16_t)ci;
+		uint32_t a_b_idx = w->n_anc;
+		for (int j = (int)c_sv->len - 1; j >= min_index;) {
+			int kmer_index = (int)c_sv->offset + j;
+			uint64_t kmer = dsb_kmer_at(bin_read + kmer_index, l_ek, ix->single_base_max);
+			uint64_t prefixValue = kmer & DSB_PRE_IDX_MASK;
+			int string_index = kmer_index + l_ek - 1;
+			int n_m = dsb_mem_search(w, bin_read + string_index, prefixValue, DSB_MEM_SEARCH_FAST,
+						 DSB_MIN_MEM_LEN_FAST - 1, string_index, &sp_set, m_r);
+			if (n_m == 0) {
+				j -= 2;
+				continue;
+			}
+			j -= 3;
+			int max_score = 0;
+			for (int k = 0; k < n_m; k++) {
+				m_r[k].read_offset = string_index - m_r[k].match_len;
+				int c_score = dsb_map_seed(w, m_r + k, &s_i);
+				max_score = DSB_MAX(c_score, max_score);
+			}
+			if (w->overflow)
+				return;
+			if (max_score > 35)
+				j -= 7;
+			if (max_score > 256) {
+				if (max_score > 512)
+					ci++;
+				break;
+			}
+		}
+		int top_score = 35;
+		for (uint32_t k = a_b_idx; k < w->n_anc; k++)
+			top_score = DSB_MAX(top_score, (int)w->anc[k].score);
+		for (uint32_t k = a_b_idx; k < w->n_anc; k++)
+			w->anc[k].anchor_useless = (w->anc[k].score < top_score) ? 1 : 0;
+	}
+}
+
+#define DSB_MEM_SEARCH_SLOW 8
+#define DSB_MIN_MEM_LEN_SLOW 20
+/* slow_classify, src/cly.c:1545-1606 */
+DSB_HDN void dsb_slow_classify(dsb_read_ws *w, const dsb_sdir_t *sd)
+{
+	const dsb_dindex_t *ix = w->ix;
+	int l_ek = ix->l_ek;
+	uint8_t *bin_read = w->bin + (sd->strand ? w->L : 0);
+	dsb_seed_t *sv_f = w->seeds + sd->seed_off;
+	dsb_spset_t sp_set = {w->spset, 0, 500};
+	dsb_mem_t *mem_rst = w->mem;
+	dsb_seedinfo_t seed_info = {bin_read, w->L, 0, sd->direction};
+	for (uint32_t i = 0; i < sd->l_seed_v_f; i++) {
+		if ((int)(sv_f[i].len) < 3 && sv_f->top == 0) /* checks seed 0's top (H10) */
+			continue;
+		int min_match_len = DSB_MIN(DSB_MIN_MEM_LEN_SLOW - 1, l_ek + 1);
+		sp_set.l = 0;
+		int mem_rst_num = 0;
+		for (int j = (int)sv_f[i].len - 1; j >= 1; j -= 2) {
+			int k_idx = (int)sv_f[i].offset + j;
+			uint64_t kmer = dsb_kmer_at(bin_read + k_idx, l_ek, ix->single_base_max);
+			uint64_t pre_v = kmer & DSB_PRE_IDX_MASK;
+			int s_idx = k_idx + l_ek - 1;
+			if (mem_rst_num + DSB_MEM_SEARCH_SLOW > 256) { /* cannot happen: seeds <= 61 long */
+				w->overflow |= 2;
+				return;
+			}
+			int c = dsb_mem_search(w, bin_read + s_idx, pre_v, DSB_MEM_SEARCH_SLOW, min_match_len, s_idx,
+					       &sp_set, mem_rst + mem_rst_num);
+			for (int k = mem_rst_num; k < mem_rst_num + c; k++)
+				mem_rst[k].read_offset = k_idx + l_ek - 1 - mem_rst[k].match_len;
+			mem_rst_num += c;
+		}
+		if (mem_rst_num == 0)
+			continue;
+		if (mem_rst_num > 1) {
+			/* qsort by match_len descending (MEM_rst_cmp_by_match_len, :1325-1328): stable */
+			uint32_t *idx = w->sidx, *tmp = w->stmp;
+			for (int k = 0; k < mem_rst_num; k++) idx[k] = k;
+			dsb_mem_t *mr = mem_rst;
+			dsb_msort(idx, tmp, (uint32_t)mem_rst_num, [mr](uint32_t a, uint32_t b) -> int {
+				return mr[b].match_len - mr[a].match_len;
+			});
+			dsb_mem_t *scratch = (dsb_mem_t *)w->anc_tmp; /* free while not chaining */
+			for (int k = 0; k < mem_rst_num; k++) scratch[k] = mem_rst[idx[k]];
+			for (int k = 0; k < mem_rst_num; k++) mem_rst[k] = scratch[k];
+		}
+		seed_info.seed_ID = (uint16_t)i;
+		uint32_t a_b_idx = w->n_anc;
+		int max_search = DSB_MIN(mem_rst_num, DSB_MEM_SEARCH_SLOW);
+		for (int k = 0; k < max_search; k++)
+			dsb_map_seed(w, mem_rst + k, &seed_info);
+		if (w->overflow)
+			return;
+		int top_score = 35;
+		for (uint32_t k = a_b_idx; k < w->n_anc; k++)
+			top_score = DSB_MAX(top_score, (int)w->anc[k].score);
+		for (uint32_t k = a_b_idx; k < w->n_anc; k++)
+			w->anc[k].anchor_useless = (w->anc[k].score < top_score) ? 1 : 0;
+	}
+	w->fast_classify = 0;
+}
+
+/* ------------------------------------------------------------------ chaining */
+DSB_HD dsb_chain_t *dsb_push_chain(dsb_read_ws *w)
+{
+	if (w->n_hit >= w->cap.hit) {
+		w->overflow |= 4;
+		return 0;
+	}
+	return w->hit + w->n_hit++;
+}
+
+/* chain_insert_meta, src/cly.c:71-111 */
+DSB_HD void dsb_chain_insert_meta(dsb_read_ws *w, uint32_t ai, dsb_chain_t *c, int new_chain, int dis_minus)
+{
+	dsb_anchor_t *anchor = w->anc + ai;
+	uint32_t ref_l = anchor->ref_offset;
+	uint32_t ref_r = ref_l + anchor->mtch_len;
+	uint32_t read_l = anchor->index_in_read;
+	uint32_t read_r = read_l + anchor->mtch_len;
+	if (new_chain) {
+		anchor->chain_id = (uint16_t)c->chain_id;
+		anchor->pre = -1;
+		c->ref_ID = anchor->ref_ID;
+		c->direction = anchor->direction;
+		c->q_t_dis = (int32_t)(anchor->ref_offset - anchor->index_in_read);
+		c->t_st = ref_l;
+		c->t_ed = ref_r;
+		c->q_st = read_l;
+		c->q_ed = read_r;
+		c->with_top_anchor = !anchor->anchor_useless;
+		c->anchor_number = 1;
+		c->sum_score = anchor->duplicate ? 1 : (uint32_t)(int32_t)anchor->score;
+		c->indel = 0;
+		c->cur = (int32_t)ai;
+	} else {
+		anchor->chain_id = (uint16_t)c->chain_id;
+		c->with_top_anchor |= (!anchor->anchor_useless);
+		if (c->q_ed >= read_r)
+			return;
+		c->t_ed = DSB_MAX(ref_r, c->t_ed);
+		c->q_ed = read_r;
+		anchor->pre = c->cur;
+		c->cur = (int32_t)ai;
+		c->q_t_dis = (int32_t)(anchor->ref_offset - anchor->index_in_read);
+		c->indel += dis_minus;
+		c->anchor_number++;
+		c->sum_score += anchor->duplicate ? 1 : (uint32_t)(int32_t)anchor->score;
+	}
+}
+
+/* chain_insert_M2, src/cly.c:200-223 */
+DSB_HD void dsb_chain_insert_M2(dsb_read_ws *w, uint32_t ai)
+{
+	dsb_anchor_t *anchor = w->anc + ai;
+	uint8_t direction = anchor->direction;
+	uint32_t ref_ID = anchor->ref_ID;
+	int32_t dis = (int32_t)(anchor->ref_offset - anchor->index_in_read);
+	int dis_minus = 0;
+	for (uint32_t k = 0; k < w->n_hit; k++) {
+		dsb_chain_t *c_s = w->hit + k;
+		if (c_s->direction == direction && c_s->ref_ID == ref_ID &&
+		    (dis_minus = DSB_ABS(dis - c_s->q_t_dis)) < 30 &&
+		    DSB_ABS_U(c_s->t_ed, anchor->ref_offset) < 400) {
+			dsb_chain_insert_meta(w, ai, c_s, 0, dis_minus);
+			return;
+		}
+	}
+	dsb_chain_t *nc = dsb_push_chain(w);
+	if (!nc)
+		return;
+	nc->chain_id = w->n_hit - 1;
+	dsb_chain_insert_meta(w, ai, nc, 1, dis_minus);
+}
+
+/* chain_insert_M3, src/cly.c:237-322 (anchors sorted in place first, src/cly.c:242) */
+DSB_HDN void dsb_chain_insert_M3(dsb_read_ws *w)
+{
+	uint32_t n = w->n_anc;
+	dsb_anchor_t *A = w->anc;
+	{
+		uint32_t *idx = w->sidx, *tmp = w->stmp;
+		for (uint32_t k = 0; k < n; k++) idx[k] = k;
+		/* Anchor_cmp_by_chr_ID_and_pos returns only 0/1 (:225-234) */
+		dsb_msort(idx, tmp, n, [A](uint32_t ia, uint32_t ib) -> int {
+			const dsb_anchor_t *a = A + ia, *b = A + ib;
+			if (a->ref_ID != b->ref_ID) return a->ref_ID > b->ref_ID;
+			if (a->direction != b->direction) return a->direction > b->direction;
+			return a->ref_offset > b->ref_offset;
+		});
+		for (uint32_t k = 0; k < n; k++) w->anc_tmp[k] = A[idx[k]];
+		for (uint32_t k = 0; k < n; k++) A[k] = w->anc_tmp[k];
+	}
+	int *score_v = (int *)w->stmp; /* 1024 ints; stmp is free again */
+	for (uint32_t chr_st = 0; chr_st < n;) {
+		uint32_t chr_ed = chr_st + 1;
+		uint32_t ref_ID = A[chr_st].ref_ID;
+		uint32_t direction = A[chr_st].direction;
+		for (; chr_ed < n && A[chr_ed].ref_ID == ref_ID && A[chr_ed].direction == direction &&
+		       A[chr_ed].ref_offset - A[chr_ed - 1].ref_offset < 2000;
+		     chr_ed++);
+		if (chr_ed - chr_st > 1024)
+			chr_ed = chr_st + 1024;
+		int32_t max_anchor = -1;
+		int max_score = 0, anchor_max_score;
+		for (uint32_t ca = chr_st; ca < chr_ed; ca++) {
+			dsb_anchor_t *c_a = A + ca;
+			c_a->pre = -1;
+			anchor_max_score = c_a->score;
+			uint32_t max_t = c_a->ref_offset + 3;
+			uint32_t max_q = c_a->index_in_read + 3;
+			for (int64_t pi = (int64_t)ca - 1; pi >= (int64_t)chr_st; pi--) {
+				dsb_anchor_t *pre = A + pi;
+				if (pre->index_in_read + pre->mtch_len > max_q) continue;
+				if (pre->ref_offset + pre->mtch_len > max_t) continue;
+				if (pre->index_in_read + 1000 < max_q) break;
+				if (pre->ref_offset + 1000 < max_t) break;
+				int indel = (int)(pre->index_in_read - pre->ref_offset - (max_q - max_t));
+				int ABS_indel = DSB_ABS(indel);
+				if (ABS_indel > 200) continue;
+				int new_score = (int)((uint32_t)(score_v[pi - chr_st] + c_a->mtch_len - (ABS_indel >> 4)) -
+						      ((max_q - pre->index_in_read) >> 8));
+				if (new_score > anchor_max_score) {
+					anchor_max_score = new_score;
+					c_a->pre = (int32_t)pi;
+				}
+			}
+			score_v[ca - chr_st] = anchor_max_score;
+			if (max_score < anchor_max_score) {
+				max_score = anchor_max_score;
+				max_anchor = (int32_t)ca;
+			}
+		}
+		if (max_anchor < 0) { /* NULL dereference in the reference (all scores <= 0): unreachable */
+			w->overflow |= 8;
+			return;
+		}
+		int sum_INDEL = 0, anchor_number = 1;
+		int32_t pre = max_anchor;
+		int sum_score = A[max_anchor].duplicate ? 1 : A[max_anchor].score;
+		int with_top = !A[max_anchor].anchor_useless;
+		for (; A[pre].pre != -1; anchor_number++) {
+			int32_t pre_ = A[pre].pre;
+			sum_INDEL += (int)((A[pre].index_in_read - A[pre_].index_in_read) - (A[pre].ref_offset - A[pre_].ref_offset));
+			with_top |= !A[pre].anchor_useless;
+			sum_score += A[pre].duplicate ? 1 : A[pre].score;
+			pre = pre_;
+		}
+		dsb_chain_t *nc = dsb_push_chain(w);
+		if (!nc)
+			return;
+		nc->chain_id = w->n_hit - 1;
+		nc->ref_ID = ref_ID;
+		nc->direction = (uint8_t)direction;
+		nc->q_t_dis = (int32_t)(A[max_anchor].ref_offset - A[max_anchor].index_in_read);
+		nc->t_st = A[pre].ref_offset;
+		nc->t_ed = A[max_anchor].ref_offset + A[max_anchor].mtch_len;
+		nc->q_st = A[pre].index_in_read;
+		nc->q_ed = A[max_anchor].index_in_read + A[max_anchor].mtch_len;
+		nc->with_top_anchor = (uint8_t)with_top;
+		nc->anchor_number = anchor_number;
+		nc->sum_score = sum_score;
+		nc->indel = sum_INDEL;
+		nc->cur = max_anchor;
+		chr_st = chr_ed;
+	}
+}
+
+/* chain_cmp_by_score, src/cly.c:37-51 */
+DSB_HD int dsb_chain_cmp_by_score(const dsb_chain_t *a, const dsb_chain_t *b)
+{
+	if (a->with_top_anchor != b->with_top_anchor)
+		return a->with_top_anchor ? -1 : 1;
+	int score_a = (int)(a->sum_score + ((a->q_ed - a->q_st) << 1));
+	score_a -= (int)(a->indel << 2);
+	int score_b = (int)(b->sum_score + ((b->q_ed - b->q_st) << 1));
+	score_b -= (int)(b->indel << 2);
+	if (score_a < score_b) return 1;
+	if (score_a > score_b) return -1;
+	return 0;
+}
+
+/* sort the chain vector in place with one of the reference comparators */
+template <typename Cmp>
+DSB_HD void dsb_sort_chains(dsb_read_ws *w, Cmp cmp)
+{
+	uint32_t n = w->n_hit;
+	if (n <= 1)
+		return;
+	uint32_t *idx = w->sidx, *tmp = w->stmp;
+	for (uint32_t k = 0; k < n; k++) idx[k] = k;
+	dsb_chain_t *H = w->hit;
+	dsb_msort(idx, tmp, n, [H, cmp](uint32_t a, uint32_t b) -> int { return cmp(H + a, H + b); });
+	for (uint32_t k = 0; k < n; k++) w->hit_tmp[k] = H[idx[k]];
+	for (uint32_t k = 0; k < n; k++) H[k] = w->hit_tmp[k];
+}
+
+/* resolve_tree, src/cly.c:325-348 */
+DSB_HDN void dsb_resolve_tree(dsb_read_ws *w)
+{
+	w->n_hit = 0;
+	if (w->n_anc < 50)
+		for (uint32_t k = 0; k < w->n_anc; k++)
+			dsb_chain_insert_M2(w, k);
+	else
+		dsb_chain_insert_M3(w);
+	if (w->overflow)
+		return;
+	if (w->n_hit > 1)
+		dsb_sort_chains(w, [](const dsb_chain_t *a, const dsb_chain_t *b) -> int { return dsb_chain_cmp_by_score(a, b); });
+	uint32_t rst_num = DSB_MIN(5u, w->n_hit);
+	while (rst_num < w->n_hit && w->hit[rst_num].with_top_anchor == 1)
+		rst_num++;
+	w->n_hit = rst_num;
+}
+
+/* ------------------------------------------------------------------ scoring (M2) */
+#define DSB_S_A_KMER_L 9
+#define DSB_MIN_SCORE_MEM 12
+#define DSB_OVER_SEARCH 50
+#define DSB_MAX_SMS_OVERLAP 6
+
+/* sc_hash_idx, src/cly.c:1686-1705 */
+DSB_HD void dsb_sc_hash_idx(dsb_read_ws *w)
+{
+	dsb_sch_t *sc = w->sch;
+	for (int k = 0; k < 256; k++) { sc[k].next = 0; sc[k].seed_ID_s_or_e = 0; }
+	int sc_con_index = 256;
+	for (uint32_t h = 0; h < w->n_hit; h++) {
+		dsb_chain_t *c_h = w->hit + h;
+		for (int i = 1; i >= 0; i--) {
+			uint16_t c_key = (uint16_t)(((i == 1) ? (c_h->t_st - c_h->q_st) : (c_h->t_ed - c_h->q_ed)) & 0xff);
+			while (sc[c_key].next != 0)
+				c_key = sc[c_key].next;
+			/* seed_ID:15 low bits, s_or_e:1 high bit (gcc bitfield order) */
+			sc[c_key].seed_ID_s_or_e = (uint16_t)(((h + 1) & 0x7fff) | ((uint32_t)i << 15));
+			sc[c_key].next = (uint16_t)sc_con_index;
+			sc[sc_con_index++].next = 0;
+		}
+	}
+}
+
+/* build_hash_table_M2, src/cly.c:2168-2219: chained 9-mer hash of the read, per strand.
+ * Chains keep insertion (= position) order, so heads/tails/next arrays reproduce the
+ * reference's lookup order exactly. */
+DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
+{
+	int both_dir = 0;
+	for (uint32_t i = 0; i < w->n_hit; i++) {
+		both_dir |= (w->hit[i].direction == DSB_FORWARD) ? 0x2 : 0x1;
+		if (both_dir == 3)
+			break;
+	}
+	int key_len = 10;
+	for (; key_len < 18; key_len++)
+		if ((int64_t)(1u << key_len) >= q_len)
+			break;
+	uint32_t KEY_MASK = (1u << key_len) - 1;
+	for (int c_dir = 2; c_dir >= 1; c_dir--) {
+		if ((c_dir & both_dir) == 0)
+			continue;
+		uint32_t direction = (c_dir == 1) ? DSB_REVERSE : DSB_FORWARD;
+		const dsb_sdir_t *csd = (w->sd[0].direction == direction) ? &w->sd[0] : &w->sd[1];
+		int h = (c_dir == 2) ? 0 : 1;
+		uint32_t *heads = w->hh[h], *tails = w->ht[h], *next = w->hn[h], *kk = w->hk[h];
+		for (uint32_t k = 0; k <= KEY_MASK; k++) heads[k] = 0xffffffffu;
+		const uint8_t *q = w->bin + (csd->strand ? w->L : 0);
+		uint32_t kmer = 0;
+		for (int k = 0; k < DSB_S_A_KMER_L - 1; k++) kmer = (kmer << 2) | q[k];
+		for (uint32_t c_pos = 0; c_pos < (uint32_t)(q_len - DSB_S_A_KMER_L + 1); c_pos++) {
+			kmer = ((kmer << 2) | q[c_pos + DSB_S_A_KMER_L - 1]) & 0x3ffff;
+			uint32_t key = kmer & KEY_MASK;
+			kk[c_pos] = kmer;
+			next[c_pos] = 0xffffffffu;
+			if (heads[key] == 0xffffffffu) heads[key] = c_pos;
+			else next[tails[key]] = c_pos;
+			tails[key] = c_pos;
+		}
+	}
+	return key_len;
+}
+
+DSB_HD dsb_spd_t *dsb_push_sms(dsb_read_ws *w)
+{
+	if (w->n_sms >= w->cap.sms) {
+		w->overflow |= 16;
+		return 0;
+	}
+	return w->sms + w->n_sms++;
+}
+
+/* MEM_search, src/cly.c:1805-1813 */
+DSB_HD int dsb_MEM_search(const uint8_t *q, const uint8_t *t, int forward, int max)
+{
+	int len = 0;
+	if (forward)
+		for (; len < max && *q++ == *t++; len++);
+	else
+		for (; len < max && *q-- == *t--; len++);
+	return len;
+}
+
+/* sdp_match, src/cly.c:2330-2435.  q_str: read buffer; t_str: reference window. */
+DSB_HDN void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const uint8_t *q_str, const uint8_t *t_str,
+			    uint32_t t_len, int key_len, int hslot, uint32_t t_st, int isForward)
+{
+	uint32_t KEY_MASK = (1u << key_len) - 1;
+	uint32_t t_kmer_num = t_len - DSB_S_A_KMER_L + 1;
+	const uint32_t *heads = w->hh[hslot], *next = w->hn[hslot], *kk = w->hk[hslot];
+	if (isForward) {
+		const uint8_t *c_t_str = t_str + 4;
+		uint64_t kmer = 0;
+		for (int k = 0; k < DSB_S_A_KMER_L; k++) kmer = (kmer << 2) | c_t_str[k];
+		kmer >>= 2;
+		for (int i = 4; i < (int)t_kmer_num; i++, c_t_str++) {
+			kmer = ((kmer << 2) | c_t_str[DSB_S_A_KMER_L - 1]) & 0x3ffff;
+			if ((i & 0x03) != 0)
+				continue;
+			for (uint32_t nd = heads[kmer & KEY_MASK]; nd != 0xffffffffu; nd = next[nd]) {
+				if (kk[nd] != (uint32_t)kmer)
+					continue;
+				uint32_t q_pos = nd;
+				if (q_pos >= q_bg && q_pos <= q_ed) {
+					int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, 4);
+					if (back_len < 4 || i == 4) {
+						uint32_t max_search = q_ed - q_pos - 1;
+						max_search = DSB_MIN(max_search, t_len - i - 1) + DSB_OVER_SEARCH;
+						int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L, 1,
+										 (int)max_search);
+						int total_len = back_len + forward_len + 1;
+						if (total_len >= 4) {
+							dsb_spd_t *p = dsb_push_sms(w);
+							if (!p) return;
+							p->len = total_len;
+							p->q_pos = q_pos - back_len;
+							p->t_pos = i - back_len + t_st;
+						}
+					}
+				}
+			}
+		}
+	} else {
+		const uint8_t *c_t_str = t_str + t_len - DSB_S_A_KMER_L - 4;
+		uint64_t kmer = 0;
+		for (int k = 0; k < DSB_S_A_KMER_L; k++) kmer = (kmer << 2) | c_t_str[k];
+		kmer <<= 2;
+		for (int i = 4; i < (int)t_kmer_num; i++, c_t_str--) {
+			kmer = (kmer >> 2) | ((uint64_t)c_t_str[0] << 16); /* bit2_preKmerMOVE, no mask */
+			if ((i & 0x03) != 0)
+				continue;
+			for (uint32_t nd = heads[kmer & KEY_MASK]; nd != 0xffffffffu; nd = next[nd]) {
+				if ((uint64_t)kk[nd] != kmer)
+					continue;
+				uint32_t q_pos = nd;
+				if (q_pos >= q_bg && q_pos <= q_ed) {
+					int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L, 1, 4);
+					if (forward_len < 4 || i == 4) {
+						uint32_t max_search = q_pos;
+						max_search = DSB_MIN(max_search, (uint32_t)(c_t_str - t_str)) + DSB_OVER_SEARCH;
+						int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, (int)max_search);
+						int total_len = back_len + forward_len + 1;
+						if (total_len >= 4) {
+							dsb_spd_t *p = dsb_push_sms(w);
+							if (!p) return;
+							p->len = total_len;
+							p->q_pos = q_pos - back_len;
+							p->t_pos = (uint32_t)(c_t_str - t_str) - back_len + t_st;
+						}
+					}
+				}
+			}
+		}
+	}
+}
+
+/* sdp_middle_M2, src/cly.c:2439-2525 */
+DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, int hslot, int key_len)
+{
+	const dsb_dindex_t *ix = w->ix;
+	int score = 10000;
+	if (c_a_i < 0)
+		return score - 10000;
+	uint64_t t_offset = ix->ref_seq_offset[w->anc[c_a_i].ref_ID];
+	while (c_a_i >= 0) {
+		dsb_anchor_t *c_a = w->anc + c_a_i;
+		int32_t pre_i = c_a->pre;
+		if (pre_i >= 0) {
+			dsb_anchor_t *pre_a = w->anc + pre_i;
+			int pre_mch = pre_a->mtch_len;
+			int pre_refoffset = (int)(pre_a->ref_offset - 3);
+			int total_ref_len = (int)(c_a->ref_offset - (uint32_t)(pre_refoffset + pre_mch) + 3);
+			w->n_sms = 0;
+			dsb_spd_t *p = dsb_push_sms(w);
+			if (!p) return 0;
+			p->score = score;
+			p->q_pos = pre_a->index_in_read;
+			p->t_pos = pre_a->ref_offset;
+			p->len = pre_a->mtch_len - DSB_S_A_KMER_L + 1;
+			if (total_ref_len > 12) {
+				/* uint8_t ref[2000] (src/cly.c:2467), pattern-initialised per entry */
+				uint8_t *ref = w->win + DSB_WIN_MID;
+				if (total_ref_len >= 2000) { /* xassert(total_ref_len < 2000) exits the reference */
+					w->overflow |= 32;
+					return 0;
+				}
+				dsb_get_ref(ix, ref, (uint64_t)(int64_t)(pre_refoffset + pre_mch) + t_offset, (uint32_t)total_ref_len, 1);
+				for (int k = total_ref_len; k < 2000 + 64; k++) ref[k] = DSB_STACK_PATTERN;
+				dsb_sdp_match(w, pre_a->index_in_read + pre_mch - 8, c_a->index_in_read - 1, q_str, ref,
+					      (uint32_t)total_ref_len, key_len, hslot, (uint32_t)(pre_refoffset + pre_mch), 1);
+				if (w->overflow) return 0;
+			}
+			p = dsb_push_sms(w);
+			if (!p) return 0;
+			p->q_pos = c_a->index_in_read;
+			p->t_pos = c_a->ref_offset;
+			p->len = c_a->mtch_len - DSB_S_A_KMER_L + 1;
+			if (w->n_sms > 1) {
+				for (uint32_t cs = 1; cs < w->n_sms; cs++) {
+					dsb_spd_t *c_spd = w->sms + cs;
+					int max_score = (int)c_spd->len;
+					uint32_t max_q = c_spd->q_pos + DSB_MAX_SMS_OVERLAP;
+					uint32_t max_t = c_spd->t_pos + DSB_MAX_SMS_OVERLAP;
+					for (int64_t ps = (int64_t)cs - 1; ps >= 0; ps--) {
+						dsb_spd_t *c_pre = w->sms + ps;
+						int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
+						int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
+						if ((uint32_t)pre_q_ed > max_q) continue; /* int vs uint32 */
+						if ((uint32_t)pre_t_ed > max_t) continue;
+						int indel = (int)(c_pre->q_pos - c_pre->t_pos - (max_q - max_t));
+						int ABS_indel = DSB_ABS(indel);
+						if (ABS_indel > 200) continue;
+						int new_score = (int)(c_pre->score + c_spd->len - (uint32_t)(ABS_indel >> 3));
+						if ((uint32_t)pre_q_ed > c_spd->q_pos || (uint32_t)pre_t_ed > c_spd->t_pos) {
+							int overlap_q = pre_q_ed - (int)c_spd->q_pos;
+							int overlap_t = pre_t_ed - (int)c_spd->t_pos;
+							new_score -= DSB_MAX(overlap_q, overlap_t);
+						}
+						max_score = DSB_MAX(max_score, new_score);
+					}
+					score = DSB_MAX(max_score, score);
+					c_spd->score = (uint32_t)max_score;
+				}
+			}
+		} else
+			score += c_a->mtch_len - DSB_S_A_KMER_L + 1;
+		c_a_i = pre_i;
+	}
+	return score - 10000;
+}
+
+/* combine_chain, src/cly.c:1758-1803 */
+DSB_HD int dsb_combine_chain(dsb_read_ws *w, int chain_ID, int dis, int isleft, int c_q_pos, int32_t *combined)
+{
+	uint16_t key = (uint16_t)(dis & 0xff);
+	dsb_chain_t *c_h = w->hit + chain_ID;
+	dsb_sch_t *sc = w->sch;
+	while (sc[key].next != 0) {
+		uint16_t seed_ID = sc[key].seed_ID_s_or_e & 0x7fff;
+		int s_or_e = sc[key].seed_ID_s_or_e >> 15;
+		dsb_chain_t *c = w->hit + seed_ID - 1;
+		int dis_con = isleft ? (int)(c->t_ed - c->q_ed) : (int)(c->t_st - c->q_st);
+		int q_pos_con = (!isleft) ? (int)c->q_st : (int)(c->q_ed - DSB_S_A_KMER_L);
+		if (dis == dis_con && c_h != c && isleft != s_or_e && DSB_ABS_U(c_q_pos, q_pos_con) < 8 &&
+		    c_h->ref_ID == c->ref_ID && c_h->direction == c->direction && c->sum_score != 0 &&
+		    (int)seed_ID - 1 > chain_ID) {
+			c_h->sum_score += c->sum_score;
+			c_h->anchor_number += c->anchor_number;
+			c_h->indel += c->indel;
+			c_h->q_st = DSB_MIN(c_h->q_st, c->q_st);
+			c_h->t_st = DSB_MIN(c_h->t_st, c->t_st);
+			c_h->q_ed = DSB_MAX(c_h->q_ed, c->q_ed);
+			c_h->t_ed = DSB_MAX(c_h->t_ed, c->t_ed);
+			c->sum_score = 0;
+			c->t_st = c->t_ed = c->q_st = c->q_ed = 0;
+			*combined = seed_ID - 1;
+			return 1;
+		}
+		key = sc[key].next;
+	}
+	return 0;
+}
+
+/* sdp_right_M2, src/cly.c:2527-2672 */
+DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int key_len, int chain_ID,
+			   uint32_t l_read, int score_ori)
+{
+	const dsb_dindex_t *ix = w->ix;
+	score_ori += 10000;
+	int total_max_score = score_ori;
+	int max_sms_id = 0;
+	dsb_chain_t *c_h = w->hit + chain_ID;
+	int32_t combined;
+	w->n_sms = 0;
+	uint8_t *ref = w->win + DSB_WIN_RL; /* uint8_t ref[1000] (src/cly.c:2537) */
+	for (int k = -64; k < 1000 + 64; k++) ref[k] = DSB_STACK_PATTERN; /* ref[-1] is read by sdp_left's back extension */
+	dsb_spd_t *p = dsb_push_sms(w);
+	if (!p) return 0;
+	p->score = score_ori;
+	p->q_pos = c_h->q_ed;
+	p->t_pos = c_h->t_ed;
+	p->len = 1 - DSB_S_A_KMER_L;
+	uint32_t current_sms = 1;
+	uint64_t t_offset_global = ix->ref_seq_offset[c_h->ref_ID];
+	uint64_t t_length = ix->ref_seq_l[c_h->ref_ID];
+	uint32_t c_t_offset = c_h->t_ed - 3;
+	int last_search = 0;
+	while (1) {
+		if (w->n_sms == current_sms) {
+			uint32_t next_step = (uint32_t)(t_length - c_t_offset);
+			if (next_step < DSB_MIN_SCORE_MEM)
+				break;
+			uint32_t max_search_ref;
+			if (l_read - c_h->q_ed < 600) {
+				if (last_search)
+					break;
+				last_search = 1;
+				max_search_ref = l_read - c_h->q_ed + 60;
+			} else
+				max_search_ref = (uint32_t)(t_length - c_t_offset);
+			max_search_ref = DSB_MIN(600u, max_search_ref);
+			dsb_get_ref(ix, ref, c_t_offset + t_offset_global, max_search_ref + DSB_OVER_SEARCH, 1);
+			int search_q_ed = (int)w->sms[max_sms_id].q_pos + 1000;
+			search_q_ed = DSB_MIN(search_q_ed, l_read);                /* int vs uint32: unsigned */
+			int search_q_st = DSB_MAX(search_q_ed - 2000, c_h->q_st - 8); /* idem (H11) */
+			dsb_sdp_match(w, (uint32_t)search_q_st, (uint32_t)search_q_ed, q_str, ref, max_search_ref, key_len, hslot,
+				      c_t_offset, 1);
+			if (w->overflow) return 0;
+			c_t_offset += max_search_ref - DSB_S_A_KMER_L - 3;
+			if (w->n_sms == current_sms)
+				break;
+			if (w->sms[current_sms].t_pos > w->sms[max_sms_id].t_pos + 1000)
+				break;
+		}
+		dsb_spd_t *c_sms = w->sms + current_sms++;
+		int max_score = (int)c_sms->len;
+		uint32_t max_pre_q = c_sms->q_pos + DSB_MAX_SMS_OVERLAP;
+		uint32_t max_pre_t = c_sms->t_pos + DSB_MAX_SMS_OVERLAP;
+		for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
+			dsb_spd_t *c_pre = w->sms + ps;
+			int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
+			int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
+			if ((uint32_t)pre_q_ed > max_pre_q) continue; /* int vs uint32 */
+			if ((uint32_t)pre_t_ed > max_pre_t) continue;
+			if (c_pre->t_pos + 600 < max_pre_t) break;
+			int indel = (int)(c_pre->q_pos - c_pre->t_pos - (max_pre_q - max_pre_t));
+			int ABS_indel = DSB_ABS(indel);
+			if (ABS_indel > 200) continue;
+			int new_score = (int)(c_pre->score + c_sms->len - (uint32_t)(ABS_indel >> 3));
+			if ((uint32_t)pre_q_ed > c_sms->q_pos || (uint32_t)pre_t_ed > c_sms->t_pos) {
+				int overlap_q = pre_q_ed - (int)c_sms->q_pos;
+				int overlap_t = pre_t_ed - (int)c_sms->t_pos;
+				new_score -= DSB_MAX(overlap_q, overlap_t);
+			}
+			max_score = DSB_MAX(max_score, new_score);
+		}
+		c_sms->score = (uint32_t)max_score;
+		if (c_sms->len >= 8 &&
+		    dsb_combine_chain(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 0, (int)c_sms->q_pos, &combined)) {
+			total_max_score = DSB_MAX(score_ori, max_score) - (int)c_sms->len +
+					  dsb_sdp_middle(w, w->hit[combined].cur, q_str, hslot, key_len);
+			if (w->overflow) return 0;
+			score_ori = total_max_score;
+			max_sms_id = 0;
+			w->n_sms = 0;
+			p = dsb_push_sms(w);
+			if (!p) return 0;
+			p->score = total_max_score;
+			p->q_pos = c_h->q_ed;
+			p->t_pos = c_h->t_ed;
+			p->len = (uint32_t)(-DSB_S_A_KMER_L);
+			current_sms = 1;
+			c_t_offset = c_h->t_ed;
+			continue;
+		}
+		if (total_max_score < max_score) {
+			total_max_score = max_score;
+			max_sms_id = current_sms - 1;
+		}
+		if (c_sms->t_pos > w->sms[max_sms_id].t_pos + 1000)
+			break;
+	}
+	c_h->q_ed = w->sms[max_sms_id].q_pos + w->sms[max_sms_id].len + DSB_S_A_KMER_L;
+	c_h->t_ed = w->sms[max_sms_id].t_pos + w->sms[max_sms_id].len + DSB_S_A_KMER_L;
+	return total_max_score - 10000;
+}
+
+/* sdp_left_M2, src/cly.c:2674-2814 (the first node's len is not written: H6) */
+DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int key_len, int chain_ID,
+			  uint32_t l_read, int score_ori)
+{
+	const dsb_dindex_t *ix = w->ix;
+	(void)l_read;
+	score_ori += 10000;
+	int total_max_score = score_ori;
+	int max_sms_id = 0;
+	dsb_chain_t *c_h = w->hit + chain_ID;
+	int32_t combined;
+	w->n_sms = 0;
+	uint8_t *ref = w->win + DSB_WIN_RL; /* uint8_t ref[1000] (src/cly.c:2683) */
+	for (int k = -64; k < 1000 + 64; k++) ref[k] = DSB_STACK_PATTERN; /* ref[-1] is read by sdp_left's back extension */
+	dsb_spd_t *p = dsb_push_sms(w);
+	if (!p) return 0;
+	p->score = score_ori;
+	p->q_pos = c_h->q_st;
+	p->t_pos = c_h->t_st;
+	uint32_t current_sms = 1;
+	uint64_t t_offset_global = ix->ref_seq_offset[c_h->ref_ID];
+	uint32_t c_t_offset = c_h->t_st + 3;
+	int last_search = 0;
+	while (1) {
+		if (w->n_sms == current_sms) {
+			uint32_t next_step = c_t_offset;
+			if (next_step < DSB_MIN_SCORE_MEM)
+				break;
+			uint32_t max_search_ref;
+			if (c_h->q_st < 600) {
+				if (last_search)
+					break;
+				last_search = 1;
+				max_search_ref = c_h->q_st + 60;
+			} else
+				max_search_ref = c_t_offset;
+			max_search_ref = DSB_MIN(600u, max_search_ref);
+			if (t_offset_global == 0 && c_t_offset < DSB_OVER_SEARCH + max_search_ref)
+				dsb_get_ref(ix, ref, c_t_offset + t_offset_global - max_search_ref, max_search_ref, 1);
+			else
+				dsb_get_ref(ix, ref, c_t_offset + t_offset_global - max_search_ref - DSB_OVER_SEARCH,
+					    max_search_ref + DSB_OVER_SEARCH, 1);
+			int search_q_st = (int)w->sms[max_sms_id].q_pos - 1000;
+			search_q_st = DSB_MAX(search_q_st, 0);
+			int search_q_ed = DSB_MIN(search_q_st + 2000, c_h->q_st - 1); /* int vs uint32: unsigned */
+			dsb_sdp_match(w, (uint32_t)search_q_st, (uint32_t)search_q_ed, q_str, ref + DSB_OVER_SEARCH, max_search_ref,
+				      key_len, hslot, c_t_offset - max_search_ref, 0);
+			if (w->overflow) return 0;
+			c_t_offset = c_t_offset - max_search_ref + DSB_S_A_KMER_L + 3;
+			if (w->n_sms == current_sms)
+				break;
+			if (w->sms[current_sms].t_pos + 1000 < w->sms[max_sms_id].t_pos)
+				break;
+		}
+		dsb_spd_t *c_sms = w->sms + current_sms++;
+		int max_score = (int)c_sms->len;
+		uint32_t min_pre_q = c_sms->q_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
+		uint32_t min_pre_t = c_sms->t_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
+		for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
+			dsb_spd_t *c_pre = w->sms + ps;
+			if (c_pre->q_pos < min_pre_q) continue;
+			if (c_pre->t_pos < min_pre_t) continue;
+			if (min_pre_t + 600 < c_pre->t_pos) break;
+			int indel = (int)(c_pre->q_pos - c_pre->t_pos - (min_pre_q - min_pre_t));
+			int ABS_indel = DSB_ABS(indel);
+			if (ABS_indel > 200) continue;
+			int new_score = (int)(c_pre->score + c_sms->len - (uint32_t)(ABS_indel >> 3));
+			if (min_pre_q + DSB_MAX_SMS_OVERLAP > c_pre->q_pos || min_pre_t + DSB_MAX_SMS_OVERLAP > c_pre->t_pos) {
+				int overlap_q = (int)(min_pre_q + DSB_MAX_SMS_OVERLAP - c_pre->q_pos);
+				int overlap_t = (int)(min_pre_t + DSB_MAX_SMS_OVERLAP - c_pre->t_pos);
+				new_score -= DSB_MAX(overlap_q, overlap_t);
+			}
+			max_score = DSB_MAX(max_score, new_score);
+		}
+		c_sms->score = (uint32_t)max_score;
+		if (c_sms->len >= 8 && dsb_combine_chain(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 1,
+							 (int)(c_sms->q_pos + c_sms->len), &combined)) {
+			total_max_score = DSB_MAX(score_ori, max_score) - (int)c_sms->len +
+					  dsb_sdp_middle(w, w->hit[combined].cur, q_str, hslot, key_len);
+			if (w->overflow) return 0;
+			score_ori = total_max_score;
+			max_sms_id = 0;
+			w->n_sms = 0;
+			p = dsb_push_sms(w);
+			if (!p) return 0;
+			p->score = total_max_score;
+			p->q_pos = c_h->q_st;
+			p->t_pos = c_h->t_st;
+			current_sms = 1;
+			c_t_offset = c_h->t_st;
+			continue;
+		}
+		if (total_max_score < max_score) {
+			total_max_score = max_score;
+			max_sms_id = current_sms - 1;
+		}
+		if (c_sms->t_pos + 1000 < w->sms[max_sms_id].t_pos)
+			break;
+	}
+	c_h->q_st = w->sms[max_sms_id].q_pos;
+	c_h->t_st = w->sms[max_sms_id].t_pos;
+	return total_max_score - 10000;
+}
+
+/* get_score_M2, src/cly.c:2816-2844 */
+DSB_HDN void dsb_get_score(dsb_read_ws *w, uint32_t l_read)
+{
+	int key_len = dsb_build_hash_table(w, (int)l_read);
+	for (uint32_t i = 0; i < w->n_hit; i++) {
+		if (w->hit[i].sum_score == 0)
+			continue;
+		const dsb_sdir_t *csd = (w->sd[0].direction == w->hit[i].direction) ? &w->sd[0] : &w->sd[1];
+		int hslot = (w->hit[i].direction == DSB_FORWARD) ? 0 : 1;
+		const uint8_t *q_str = w->bin + (csd->strand ? w->L : 0);
+		int score = dsb_sdp_middle(w, w->hit[i].cur, q_str, hslot, key_len);
+		if (w->overflow) return;
+		score = dsb_sdp_right(w, q_str, hslot, key_len, (int)i, l_read, score);
+		if (w->overflow) return;
+		score = dsb_sdp_left(w, q_str, hslot, key_len, (int)i, l_read, score);
+		if (w->overflow) return;
+		w->hit[i].sum_score = (uint32_t)score;
+	}
+}
+
+/* chain_cmp_by_pos, src/cly.c:2848-2865 */
+DSB_HD int dsb_chain_cmp_by_pos(const dsb_chain_t *a, const dsb_chain_t *b)
+{
+	if (a->ref_ID > b->ref_ID) return 1;
+	if (a->ref_ID < b->ref_ID) return -1;
+	if (a->t_st > b->t_st) return 1;
+	if (a->t_st < b->t_st) return -1;
+	if (a->sum_score < b->sum_score) return 1;
+	if (a->sum_score > b->sum_score) return -1;
+	return 0;
+}
+
+/* chain_cmp_by_MEM_score, src/cly.c:53-63 (ties return a->sum_score % 2: H9) */
+DSB_HD int dsb_chain_cmp_by_MEM_score(const dsb_chain_t *a, const dsb_chain_t *b)
+{
+	int score_a = (int)(a->sum_score << 5);
+	int score_b = (int)(b->sum_score << 5);
+	if (score_a < score_b) return 1;
+	if (score_a > score_b) return -1;
+	return (int)(a->sum_score % 2);
+}
+
+/* delete_small_score_rst, src/cly.c:2878-2952 — part A (up to the max_read_l update) */
+DSB_HDN void dsb_delete_small_A(dsb_read_ws *w)
+{
+	w->reached_update = 0;
+	if (w->n_hit == 0)
+		return;
+	if (w->n_hit > 200) {
+		uint32_t rst_num = 200;
+		for (; rst_num < w->n_hit && w->hit[rst_num].sum_score > 50; rst_num++);
+		w->n_hit = rst_num;
+	}
+	w->n_hit = DSB_MIN(400u, w->n_hit);
+	uint32_t l_read = w->L;
+	dsb_sc_hash_idx(w);
+	dsb_get_score(w, l_read);
+	if (w->overflow)
+		return;
+	uint32_t n = w->n_hit;
+	if (n > 1)
+		dsb_sort_chains(w, [](const dsb_chain_t *a, const dsb_chain_t *b) -> int { return dsb_chain_cmp_by_pos(a, b); });
+	dsb_chain_t *H = w->hit;
+	for (uint32_t ci = 0; n > 0 && ci < n - 1; ci++) {
+		dsb_chain_t *c_c = H + ci;
+		if (c_c->sum_score == 0)
+			continue;
+		for (uint32_t ni = ci + 1; ni < n; ni++) {
+			dsb_chain_t *next_c = H + ni;
+			if (c_c->ref_ID == next_c->ref_ID) {
+				if (c_c->direction != next_c->direction)
+					continue;
+				if (next_c->sum_score == 0)
+					continue;
+				if (next_c->t_st < c_c->t_st + 5 && next_c->q_st < c_c->q_st + 5 &&
+				    next_c->sum_score < c_c->sum_score + 5) {
+					next_c->sum_score = 0;
+					next_c->q_ed = next_c->q_st;
+					next_c->t_ed = next_c->t_st;
+					continue;
+				}
+				int dis_t = (int)(next_c->t_st - c_c->t_ed);
+				int dis_q = (int)(next_c->q_st - c_c->q_ed);
+				int dis_t_q = DSB_ABS(dis_t - dis_q);
+				if ((dis_t > -20 && dis_t < 1000 && dis_q > -20 && dis_q < 1000) && dis_t_q < 200) {
+					c_c->t_ed = DSB_MAX(c_c->t_ed, next_c->t_ed);
+					c_c->q_ed = DSB_MAX(c_c->q_ed, next_c->q_ed);
+					c_c->sum_score += next_c->sum_score;
+					next_c->sum_score = 0;
+					next_c->q_ed = next_c->q_st;
+					next_c->t_ed = next_c->t_st;
+				}
+			} else
+				break;
+		}
+	}
+	w->reached_update = 1;
+}
+
+/* delete_small_score_rst part B (src/cly.c:2953-2987) + detect_primary (src/cly.c:2990-3053);
+ * max_read_l is the carried pool value already including this read (H2). */
+DSB_HDN void dsb_delete_small_B(dsb_read_ws *w, int max_read_l)
+{
+	if (!w->reached_update)
+		return;
+	const dsb_dindex_t *ix = w->ix;
+	uint32_t l_read = w->L;
+	dsb_chain_t *H = w->hit;
+	uint32_t n = w->n_hit;
+	if (max_read_l < 510) {
+		for (uint32_t k = 0; k < n; k++) {
+			int score = (int)(H[k].sum_score + ((H[k].q_ed - H[k].q_st) >> 5));
+			if (score < 26) H[k].sum_score = 0;
+		}
+	} else if (l_read < 310) {
+		for (uint32_t k = 0; k < n; k++) {
+			int score = (int)(H[k].sum_score + ((H[k].q_ed - H[k].q_st) >> 5));
+			if (score < 30) H[k].sum_score = 0;
+		}
+	} else {
+		for (uint32_t k = 0; k < n; k++) {
+			int score = (int)(H[k].sum_score + ((H[k].q_ed - H[k].q_st) >> 5));
+			if (score < ix->filter_min_score_LV3 &&
+			    ((H[k].q_ed - H[k].q_st) < (uint32_t)ix->filter_min_length || score < ix->filter_min_score))
+				H[k].sum_score = 0;
+		}
+	}
+	if (n > 1)
+		dsb_sort_chains(w, [](const dsb_chain_t *a, const dsb_chain_t *b) -> int { return dsb_chain_cmp_by_MEM_score(a, b); });
+	uint32_t k = 0;
+	for (; k < n; k++)
+		if (H[k].sum_score == 0)
+			break;
+	w->n_hit = k;
+}
+
+/* detect_primary, src/cly.c:2990-3053 */
+DSB_HDN void dsb_detect_primary(dsb_read_ws *w, uint32_t read_len, int *primary_v, uint8_t *primary_v_idx)
+{
+	dsb_chain_t *hit = w->hit;
+	uint32_t n_hit = w->n_hit;
+	if (n_hit == 0)
+		return;
+	int n_primary_v = 1;
+	hit->pri_index = primary_v_idx[0] = 0;
+	primary_v[0] = 0;
+	hit->primary = 1; /* PRIMARY */
+	for (uint32_t k = 0; k < n_hit; k++)
+		if (hit[k].q_st > 4294960000u)
+			hit[k].q_st = 0;
+	for (uint32_t ci = 1; ci < n_hit; ci++) {
+		dsb_chain_t *c_hit = hit + ci;
+		int overlap = 0;
+		for (int i = 0; i < n_primary_v; i++) {
+			int primary_st, primary_ed;
+			if (hit[primary_v[i]].direction == c_hit->direction) {
+				primary_st = (int)hit[primary_v[i]].q_st;
+				primary_ed = (int)hit[primary_v[i]].q_ed;
+			} else {
+				primary_st = (int)(read_len - hit[primary_v[i]].q_ed);
+				primary_ed = (int)(read_len - hit[primary_v[i]].q_st);
+			}
+			/* MAX/MIN on uint32 vs int: compared as unsigned */
+			uint32_t overlap_st = DSB_MAX(c_hit->q_st, (uint32_t)primary_st);
+			uint32_t overlap_ed = DSB_MIN(c_hit->q_ed, (uint32_t)primary_ed);
+			if ((overlap_st < overlap_ed) && (((overlap_ed - overlap_st) << 1) >= (c_hit->q_ed - c_hit->q_st)))
+				overlap = 1;
+			if (overlap) {
+				c_hit->primary = 2; /* SECONDARY */
+				c_hit->pri_index = ++primary_v_idx[i];
+				int max_gap = DSB_MAX((int)(hit[primary_v[i]].sum_score >> 6), 5);
+				if (c_hit->sum_score + max_gap > hit[primary_v[i]].sum_score) /* uint32 + int: unsigned */
+					c_hit->pri_index = 1;
+				if (primary_v_idx[i] == 255)
+					primary_v_idx[i] = 254;
+				break;
+			}
+		}
+		if (!overlap) {
+			c_hit->primary = 3; /* SUPPLYMENTARY */
+			c_hit->pri_index = primary_v_idx[n_primary_v] = 0;
+			primary_v[n_primary_v++] = (int)ci;
+			if (n_primary_v > 750)
+				n_primary_v = 750;
+		}
+	}
+}
+
+/* classify_seq, src/cly.c:3059-3127 — part A: everything before the max_read_l update. */
+DSB_HDN void dsb_classify_A(dsb_read_ws *w)
+{
+	w->n_anc = 0;
+	w->fast_classify = 1;
+	w->n_hit = 0;
+	w->reached_update = 0;
+	if (w->L < DSB_MIN_READ_LEN)
+		return;
+	dsb_get_island(w);
+	int both_direction = ((w->sd[0].total_score - w->sd[1].total_score) <= (w->sd[0].total_score >> 3));
+	int super_repeat = 0; /* fast_classify returns super_repeat[0], never incremented */
+	dsb_fast_classify(w, &w->sd[0]);
+	if (w->overflow) return;
+	if (both_direction) {
+		dsb_fast_classify(w, &w->sd[1]);
+		if (w->overflow) return;
+	}
+	dsb_resolve_tree(w);
+	if (w->overflow) return;
+	int run_slow_mode = 0;
+	if (w->n_hit <= 0)
+		run_slow_mode = 1;
+	else if (w->hit[0].anchor_number < 5 && super_repeat < 3) {
+		run_slow_mode = 1;
+		if (w->L <= 300 && w->hit[0].sum_score > 200)
+			run_slow_mode = 0;
+	}
+	if (run_slow_mode) {
+		w->n_anc = 0;
+		dsb_slow_classify(w, &w->sd[0]);
+		if (w->overflow) return;
+		dsb_resolve_tree(w);
+		if (w->overflow) return;
+		if (both_direction || w->n_hit <= 0 || (w->hit[0].anchor_number < 5 && super_repeat < 3)) {
+			dsb_slow_classify(w, &w->sd[1]);
+			if (w->overflow) return;
+			dsb_resolve_tree(w);
+			if (w->overflow) return;
+		}
+	}
+	dsb_delete_small_A(w);
+}
+
+
+/* ------------------------------------------------------------------ finish + output */
+/* delete_small_score_rst part B + detect_primary + copy of the hits the SAM writer needs. */
+DSB_HD void dsb_classify_B(dsb_read_ws *w, int max_read_l, dsb_read_out_t *ro, dsb_hit_out_t *out, uint32_t out_cap)
+{
+	if (w->reached_update)
+		dsb_delete_small_B(w, max_read_l);
+	dsb_detect_primary(w, w->L, (int *)w->stmp, (uint8_t *)w->sidx);
+	uint32_t n = DSB_MIN(w->n_hit, out_cap);
+	for (uint32_t k = 0; k < n; k++) {
+		const dsb_chain_t *c = w->hit + k;
+		dsb_hit_out_t *o = out + k;
+		o->ref_ID = c->ref_ID;
+		o->sum_score = c->sum_score;
+		o->t_st = c->t_st; o->t_ed = c->t_ed; o->q_st = c->q_st; o->q_ed = c->q_ed;
+		o->indel = c->indel;
+		o->direction = c->direction; o->primary = c->primary; o->pri_index = c->pri_index; o->pad = 0;
+	}
+	ro->n_hit = n;
+	ro->n_anchor = w->n_anc;
+	ro->fast = w->fast_classify;
+	ro->status = w->overflow;
+	ro->reached_update = w->reached_update;
+}
+#endif /* DSB_CLASSIFY_H */

@@ -1,0 +1,115 @@
+/*
+ * tests/emu/emu_classify.cpp — TEST-ONLY kernel-logic emulation.
+ *
+ * Runs the exact per-read device code of desamba-so_amd/csrc/gpu/dsb_classify.h on the
+ * host CPU, one read after the other, so that the classify logic can be checked against
+ * the reference oracle in a container without a GPU.  It is never linked into
+ * libdesamba.so (whose classify path exists only as HIP kernels) and never used by
+ * bench.py's timed leg.
+ *
+ * usage: emu_classify [--dump-seeds] [--stats] <index_dir> <reads.fq>  > out.sam
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+extern "C" {
+#include "../../desamba-so_amd/csrc/dsb_host.h"
+}
+#include "../../desamba-so_amd/csrc/gpu/dsb_ws.h"
+
+int main(int argc, char **argv)
+{
+	int ai = 1, stats = 0, fmt = DSB_OUT_SAM_FULL;
+	for (; ai < argc && argv[ai][0] == '-'; ai++) {
+		if (!strcmp(argv[ai], "--stats")) stats = 1;
+		else if (!strcmp(argv[ai], "--des")) fmt = DSB_OUT_DES;
+		else { fprintf(stderr, "unknown option %s\n", argv[ai]); return 2; }
+	}
+	if (ai + 2 > argc) {
+		fprintf(stderr, "usage: %s [--stats] [--des] <index_dir> <reads>\n", argv[0]);
+		return 2;
+	}
+	static dsb_index ix;
+	memset(&ix, 0, sizeof(ix));
+	char err[512];
+	if (dsb_index_load_files(&ix, argv[ai], err, sizeof(err))) {
+		fprintf(stderr, "%s\n", err);
+		return 1;
+	}
+	ix.filter_min_length = 170;
+	ix.filter_min_score = 64;
+	ix.filter_min_score_LV3 = 74;
+	dsb_mapq_tables(&ix, 0.15, ix.ref_bin_n * 4);
+	dsb_dindex_t d;
+	dsb_index_host_view(&ix, &d);
+
+	char *buf;
+	uint64_t len;
+	if (dsb_slurp_path(argv[ai + 1], &buf, &len)) {
+		fprintf(stderr, "cannot read %s\n", argv[ai + 1]);
+		return 1;
+	}
+	dsb_reads_t reads;
+	memset(&reads, 0, sizeof(reads));
+	dsb_parse_reads(buf, len, &reads);
+
+	int max_read_l = 0;
+	std::vector<uint8_t> arena;
+	dsb_str out = {0, 0, 0};
+	std::vector<dsb_hit_out_t> hits(400);
+	uint64_t st[DSB_ST_N];
+	memset(st, 0, sizeof(st));
+	uint64_t n_retry = 0;
+	for (uint64_t i = 0; i < reads.n; i++) {
+		uint32_t L = reads.rec[i].seq_l;
+		const uint8_t *seq = (const uint8_t *)reads.arena + reads.rec[i].seq_off;
+		dsb_read_out_t ro;
+		for (uint32_t scale = 1;; scale *= DSB_CAP_RETRY) {
+			dsb_caps_t cap = dsb_default_caps(L, scale);
+			dsb_ws_layout lay = dsb_layout(L, cap);
+			arena.assign(lay.total + 256, 0xEE);
+			dsb_read_ws w;
+			dsb_ws_init(&w, &d, arena.data(), L, cap);
+			if (stats) w.stats = st;
+			/* encode (CLY_Bit) + reverse complement + guards (src/cly.c:1245-1254) */
+			for (uint32_t k = 0; k < L; k++) w.bin[k] = dsb_cly_bit(seq[k]);
+			for (uint32_t k = 0; k < L; k++) w.bin[L + L - 1 - k] = 3 - w.bin[k];
+			dsb_bin_guards(w.bin, L);
+			/* exist bits (K_seed) */
+			if (L >= DSB_MIN_READ_LEN) {
+				uint32_t lk = L - d.l_ek + 1;
+				uint64_t *ex[2] = {(uint64_t *)w.exF, (uint64_t *)w.exR};
+				for (int s = 0; s < 2; s++) {
+					memset(ex[s], 0, 8 * dsb_ex_words(L));
+					for (uint32_t k = 0; k < lk; k++) {
+						uint64_t km = dsb_kmer_at(w.bin + s * L + k, d.l_ek, d.single_base_max);
+						if (dsb_exist_kmer(&d, km)) ex[s][k >> 6] |= 1ull << (k & 63);
+					}
+				}
+			}
+			dsb_classify_A(&w);
+			if (w.overflow) {
+				n_retry++;
+				continue;
+			}
+			int mrl = max_read_l;
+			if (w.reached_update && (int)L > mrl) mrl = (int)L;
+			dsb_classify_B(&w, mrl, &ro, hits.data(), 400);
+			max_read_l = mrl;
+			break;
+		}
+		dsb_format_read(&out, &ix, &reads, i, &ro, hits.data(), fmt, 5);
+		if (out.l > (1 << 24)) {
+			fwrite(out.s, 1, out.l, stdout);
+			out.l = 0;
+		}
+	}
+	fwrite(out.s, 1, out.l, stdout);
+	if (stats) {
+		fprintf(stderr, "reads %lu retries %lu\n", (unsigned long)reads.n, (unsigned long)n_retry);
+		const char *nm[DSB_ST_N] = {"occ", "occ_nib", "memsearch", "sa", "uni", "refpos", "getref_b", "anchor", "chain", "ek1", "ek2"};
+		for (int k = 0; k < DSB_ST_N; k++) fprintf(stderr, "%s %lu\n", nm[k], (unsigned long)st[k]);
+	}
+	return 0;
+}
