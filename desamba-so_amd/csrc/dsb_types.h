@@ -76,7 +76,8 @@ typedef struct {
 	uint32_t fast;         /* results->fast_classify */
 	uint32_t status;       /* 0 ok; bit0 overflow (re-run with larger workspace) */
 	uint32_t reached_update; /* read reached the max_read_l update (cly.c:2953) */
-	uint32_t pad[3];
+	uint32_t pad;
+	uint64_t hit_off;      /* index of the read's first hit in the compact hit array */
 } dsb_read_out_t;
 
 #ifdef __cplusplus

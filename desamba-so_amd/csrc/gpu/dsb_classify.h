@@ -54,6 +54,22 @@ typedef struct { /* SEARCH_DIR, src/cly.c:941-949 */
 	uint32_t total_score;
 } dsb_sdir_t;
 
+/* Anchor_cmp_by_chr_ID_and_pos, src/cly.c:225-234: returns only 0/1 ("a > b"), which under
+ * glibc's merge sort is a stable ascending sort by (ref_ID, direction, ref_offset). */
+DSB_HD int dsb_anchor_cmp(const dsb_anchor_t *a, const dsb_anchor_t *b)
+{
+	int r = (a->ref_ID > b->ref_ID);
+	int d = (a->direction > b->direction);
+	int o = (a->ref_offset > b->ref_offset);
+	return (a->ref_ID != b->ref_ID) ? r : ((a->direction != b->direction) ? d : o);
+}
+
+/* MEM_rst_cmp_by_match_len, src/cly.c:1325-1328 */
+DSB_HD int dsb_mem_cmp(const dsb_mem_t *a, const dsb_mem_t *b)
+{
+	return b->match_len - a->match_len;
+}
+
 /* workspace capacities (elements) */
 typedef struct {
 	uint32_t anc, hit, sms;
@@ -650,9 +666,7 @@ DSB_HDN void dsb_slow_classify(dsb_read_ws *w, const dsb_sdir_t *sd)
 			uint32_t *idx = w->sidx, *tmp = w->stmp;
 			for (int k = 0; k < mem_rst_num; k++) idx[k] = k;
 			dsb_mem_t *mr = mem_rst;
-			dsb_msort(idx, tmp, (uint32_t)mem_rst_num, [mr](uint32_t a, uint32_t b) -> int {
-				return mr[b].match_len - mr[a].match_len;
-			});
+			dsb_msort(idx, tmp, (uint32_t)mem_rst_num, [mr](uint32_t a, uint32_t b) -> int { return dsb_mem_cmp(mr + a, mr + b); });
 			dsb_mem_t *scratch = (dsb_mem_t *)w->anc_tmp; /* free while not chaining */
 			for (int k = 0; k < mem_rst_num; k++) scratch[k] = mem_rst[idx[k]];
 			for (int k = 0; k < mem_rst_num; k++) mem_rst[k] = scratch[k];
@@ -754,13 +768,7 @@ DSB_HDN void dsb_chain_insert_M3(dsb_read_ws *w)
 	{
 		uint32_t *idx = w->sidx, *tmp = w->stmp;
 		for (uint32_t k = 0; k < n; k++) idx[k] = k;
-		/* Anchor_cmp_by_chr_ID_and_pos returns only 0/1 (:225-234) */
-		dsb_msort(idx, tmp, n, [A](uint32_t ia, uint32_t ib) -> int {
-			const dsb_anchor_t *a = A + ia, *b = A + ib;
-			if (a->ref_ID != b->ref_ID) return a->ref_ID > b->ref_ID;
-			if (a->direction != b->direction) return a->direction > b->direction;
-			return a->ref_offset > b->ref_offset;
-		});
+		dsb_msort(idx, tmp, n, [A](uint32_t ia, uint32_t ib) -> int { return dsb_anchor_cmp(A + ia, A + ib); });
 		for (uint32_t k = 0; k < n; k++) w->anc_tmp[k] = A[idx[k]];
 		for (uint32_t k = 0; k < n; k++) A[k] = w->anc_tmp[k];
 	}
@@ -1381,16 +1389,18 @@ DSB_HDN void dsb_get_score(dsb_read_ws *w, uint32_t l_read)
 	}
 }
 
-/* chain_cmp_by_pos, src/cly.c:2848-2865 */
+/* chain_cmp_by_pos, src/cly.c:2848-2865.  Written as sign differences: the early-return form
+ * of the reference is mis-scheduled by hipcc (ROCm 7.2, gfx950) inside the merge loop of
+ * dsb_msort (permutation with duplicates; tests/test_gpu_selftest.py pins it). */
 DSB_HD int dsb_chain_cmp_by_pos(const dsb_chain_t *a, const dsb_chain_t *b)
 {
-	if (a->ref_ID > b->ref_ID) return 1;
-	if (a->ref_ID < b->ref_ID) return -1;
-	if (a->t_st > b->t_st) return 1;
-	if (a->t_st < b->t_st) return -1;
-	if (a->sum_score < b->sum_score) return 1;
-	if (a->sum_score > b->sum_score) return -1;
-	return 0;
+	int c = (a->ref_ID > b->ref_ID) - (a->ref_ID < b->ref_ID);
+	if (c)
+		return c;
+	c = (a->t_st > b->t_st) - (a->t_st < b->t_st);
+	if (c)
+		return c;
+	return (a->sum_score < b->sum_score) - (a->sum_score > b->sum_score);
 }
 
 /* chain_cmp_by_MEM_score, src/cly.c:53-63 (ties return a->sum_score % 2: H9) */

@@ -1,0 +1,44 @@
+/*
+ * dsb_gpu.h — the thin C-ABI between the C host code and the HIP kernels.
+ * Plain pointers and sizes only; implemented in kernels.hip.
+ */
+#ifndef DSB_GPU_H
+#define DSB_GPU_H
+#include <stdint.h>
+#include <stddef.h>
+#include "../dsb_host.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSB_MAX_HITS 400 /* delete_small_score_rst keeps at most 400 chains (src/cly.c:2892) */
+
+typedef struct {
+	double ms_total;      /* wall time of dsb_gpu_classify, host-measured */
+	double ms_h2d, ms_d2h;
+	double ms_encode, ms_seed, ms_classA, ms_classB; /* HIP-event kernel times, summed over chunks */
+	uint64_t n_reads, n_bases, n_retry, n_chunks;
+	uint64_t seed_positions; /* k-mer positions probed by the seed kernel (both strands) */
+	uint64_t stats[16];   /* algorithmic-work counters (DSB_ST_*), when enabled */
+} dsb_gpu_timing;
+
+/* Upload the index to `device` (-1: DSB_DEVICE env var, else the current HIP device).
+ * Returns 0; on failure fills err. */
+int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn);
+void dsb_gpu_free(dsb_index *ix);
+
+/* Classify reads[0..n).  *max_read_l is the carried Classify_buff_pool.max_read_l (in/out).
+ * ro[n] receives the per-read results; *hits (malloc'd, caller frees) the compact hit records,
+ * read i owning hits[ro[i].hit_off .. + ro[i].n_hit).  stats_on: collect work counters. */
+int dsb_gpu_classify(dsb_index *ix, const dsb_reads_t *reads, int *max_read_l, dsb_read_out_t *ro,
+		     dsb_hit_out_t **hits, uint64_t *n_hits, int stats_on, dsb_gpu_timing *timing, char *err,
+		     size_t errn);
+
+/* Number of visible devices (0 if HIP has none). */
+int dsb_gpu_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

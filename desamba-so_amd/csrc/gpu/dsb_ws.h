@@ -38,7 +38,7 @@ DSB_HD uint32_t dsb_ex_words(uint32_t L) { return (L >> 6) + 2; }
 DSB_HD uint32_t dsb_seed_cap(uint32_t L) { return (L >> 1) + 20 + L / 3 + 64; }
 
 typedef struct {
-	uint64_t bin, exF, exR, seeds, anc, anc_tmp, sidx, stmp, hit, hit_tmp, sms, hash, sch, win, mem, spset, total;
+	uint64_t bin, exF, exR, seeds, anc, anc_tmp, sidx, stmp, hit, hit_tmp, sms, hash, sch, win, mem, spset, state, total;
 	uint32_t kl;
 } dsb_ws_layout;
 
@@ -64,6 +64,7 @@ DSB_HD dsb_ws_layout dsb_layout(uint32_t L, dsb_caps_t cap)
 	o.win = p; p = dsb_al(p + DSB_WIN_BYTES);
 	o.mem = p; p = dsb_al(p + sizeof(dsb_mem_t) * 256);
 	o.spset = p; p = dsb_al(p + 8 * 512);
+	o.state = p; p = dsb_al(p + 2 * sizeof(dsb_sdir_t)); /* SEARCH_DIR pair kept for diagnostics */
 	o.total = p;
 	return o;
 }

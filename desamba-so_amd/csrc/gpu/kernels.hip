@@ -1,0 +1,688 @@
+/*
+ * kernels.hip — MI355X (gfx950) kernels of the deSAMBA classify path + the launch shim
+ * behind dsb_gpu.h.
+ *
+ * Pipeline per chunk of reads (input order; chunk size set by the HBM workspace budget):
+ *   k_encode   one workgroup per read: ASCII -> 2-bit forward + reverse complement into the
+ *              read's workspace, guard bytes (src/cly.c:1245-1254)
+ *   k_seed     one wavefront per 64 consecutive k-mer positions of one strand: rolling l_ek-mer,
+ *              low-complexity filter, two-table Bloom probe (src/cly.c:359-397, 951-967),
+ *              __ballot -> one 64-bit exist word per wave (coalesced store)
+ *   k_classA   one lane per read (reads sorted by length): islands, fast/slow FM search,
+ *              map_seed, chaining, SDP rescoring (src/cly.c:3059-3124, 2878-2952)
+ *   (host)     max_read_l carry = prefix max over reads that reached cly.c:2953 (H2)
+ *   k_classB   one lane per read: length-class filter, MEM-score sort, primary detection;
+ *              hit records compacted with one atomic bump per read
+ * Reads whose dynamic vectors overflow are re-run (encode/seed/A) with 8x workspace.
+ */
+#include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <vector>
+#include <algorithm>
+#include "dsb_ws.h"
+#include "dsb_gpu.h"
+#include "dsb_debug.h"
+
+#define HIP_OK(x)                                                                                    \
+	do {                                                                                         \
+		hipError_t e_ = (x);                                                                 \
+		if (e_ != hipSuccess) {                                                              \
+			snprintf(err, errn, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+			return -1;                                                                   \
+		}                                                                                    \
+	} while (0)
+
+/* ------------------------------------------------------------------ kernels */
+__global__ __launch_bounds__(256) void k_encode(const uint8_t *__restrict__ seq, const uint64_t *__restrict__ seq_off,
+						 const uint32_t *__restrict__ len, const uint64_t *__restrict__ ws_off,
+						 uint8_t *__restrict__ ws, const uint32_t *__restrict__ sel, uint32_t n)
+{
+	uint32_t i = blockIdx.x;
+	if (i >= n)
+		return;
+	uint32_t r = sel ? sel[i] : i;
+	uint32_t L = len[r];
+	const uint8_t *s = seq + seq_off[r];
+	uint8_t *bin = ws + ws_off[r] + DSB_BIN_GUARD; /* dsb_layout(...).bin == 0 */
+	for (uint32_t k = threadIdx.x; k < L; k += blockDim.x) {
+		uint8_t b = dsb_cly_bit(s[k]);
+		bin[k] = b;
+		bin[2 * L - 1 - k] = 3 - b;
+	}
+	if (threadIdx.x < DSB_BIN_GUARD) {
+		int k = DSB_BIN_GUARD - threadIdx.x; /* bin[-k] */
+		uint8_t v = DSB_HEAP_PERTURB;
+		if (k <= 8)
+			v = (uint8_t)(dsb_chunk_header(L) >> (8 * (8 - k)));
+		bin[-k] = v;
+	}
+	for (uint32_t k = threadIdx.x; k < DSB_BIN_TAIL; k += blockDim.x)
+		bin[2ull * L + k] = DSB_HEAP_PERTURB;
+}
+
+/* one wave = 64 k-mer positions of one strand of one read */
+__global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+					       const uint64_t *__restrict__ ws_off, uint8_t *__restrict__ ws,
+					       const uint64_t *__restrict__ word_off, const uint32_t *__restrict__ sel,
+					       uint32_t n, uint64_t total_waves)
+{
+	uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+	uint32_t lane = threadIdx.x & 63;
+	if (wave >= total_waves)
+		return;
+	/* binary search: word_off[i] <= wave < word_off[i+1] */
+	uint32_t lo = 0, hi = n;
+	while (hi - lo > 1) {
+		uint32_t mid = (lo + hi) >> 1;
+		if (word_off[mid] <= wave) lo = mid; else hi = mid;
+	}
+	uint32_t r = sel ? sel[lo] : lo;
+	uint32_t L = len[r];
+	int l_ek = ix->l_ek;
+	uint32_t lk = L - l_ek + 1;
+	uint32_t nw = (lk + 63) >> 6;
+	uint64_t wi = wave - word_off[lo];
+	uint32_t strand = wi >= nw;
+	uint32_t word = (uint32_t)(strand ? wi - nw : wi);
+	uint8_t *base = ws + ws_off[r];
+	const uint8_t *bin = base + DSB_BIN_GUARD + strand * L;
+	dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, 1)); /* ex offsets do not depend on caps */
+	uint64_t *ex = (uint64_t *)(base + (strand ? lay.exR : lay.exF));
+	uint32_t k = word * 64 + lane;
+	int e = 0;
+	if (k < lk) {
+		uint64_t km = dsb_kmer_at(bin + k, l_ek, ix->single_base_max);
+		e = dsb_exist_kmer(ix, km);
+	}
+	uint64_t bits = __ballot(e);
+	if (lane == 0)
+		ex[word] = bits;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(64) void k_classA(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+						const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+						uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+						dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
+						unsigned long long *__restrict__ gstats)
+{
+	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= n)
+		return;
+	uint32_t r = order[t];
+	uint32_t L = len[r];
+	dsb_read_ws w;
+	dsb_ws_init(&w, ix, ws + ws_off[r], L, dsb_default_caps(L, scale[r]));
+	uint64_t st[DSB_ST_N];
+	if (STATS) {
+		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
+		w.stats = st;
+	}
+	dsb_classify_A(&w);
+	{
+		dsb_sdir_t *sv = (dsb_sdir_t *)(ws + ws_off[r] + dsb_layout(L, w.cap).state);
+		sv[0] = w.sd[0];
+		sv[1] = w.sd[1];
+	}
+	dsb_read_out_t o;
+	o.n_hit = w.n_hit;
+	o.n_anchor = w.n_anc;
+	o.fast = w.fast_classify;
+	o.status = w.overflow;
+	o.reached_update = w.reached_update;
+	o.pad = 0;
+	o.hit_off = 0;
+	ro[r] = o;
+	if (w.overflow)
+		atomicAdd(n_overflow, 1u);
+	if (STATS && !w.overflow)
+		for (int k = 0; k < DSB_ST_N; k++)
+			atomicAdd(gstats + k, (unsigned long long)st[k]);
+}
+
+__global__ __launch_bounds__(64) void k_classB(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+						const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+						uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+						const int32_t *__restrict__ mrl, dsb_read_out_t *__restrict__ ro,
+						dsb_hit_out_t *__restrict__ hits_out, uint32_t *__restrict__ hit_cursor,
+						uint32_t *__restrict__ hit_off)
+{
+	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= n)
+		return;
+	uint32_t r = order[t];
+	uint32_t L = len[r];
+	dsb_read_ws w;
+	dsb_ws_init(&w, ix, ws + ws_off[r], L, dsb_default_caps(L, scale[r]));
+	dsb_read_out_t o = ro[r];
+	w.n_hit = o.n_hit;
+	w.n_anc = o.n_anchor;
+	w.fast_classify = o.fast;
+	w.overflow = o.status;
+	w.reached_update = o.reached_update;
+	/* hits are staged in the read's own hit_tmp region, then compacted */
+	dsb_hit_out_t *stage = (dsb_hit_out_t *)w.hit_tmp;
+	dsb_classify_B(&w, mrl[r], &o, stage, DSB_MAX_HITS);
+	uint32_t off = atomicAdd(hit_cursor, o.n_hit);
+	for (uint32_t k = 0; k < o.n_hit; k++)
+		hits_out[off + k] = stage[k];
+	hit_off[r] = off;
+	o.hit_off = off;
+	ro[r] = o;
+}
+
+/* The merge-sort orders the classifier depends on, one array per lane:
+ * which 0 chain_cmp_by_pos, 1 chain_cmp_by_MEM_score, 2 chain_cmp_by_score, 3 anchors
+ * (Anchor_cmp_by_chr_ID_and_pos), 4 MEM_rst by match_len.  Output: permutation in idx. */
+DSB_HD void dsb_selftest_one(dsb_chain_t *H, dsb_chain_t *T, uint32_t *idx, uint32_t *tmpi, uint32_t n, int which)
+{
+	for (uint32_t k = 0; k < n; k++) idx[k] = k;
+	if (which == 0)
+		dsb_msort(idx, tmpi, n, [H](uint32_t a, uint32_t b) -> int { return dsb_chain_cmp_by_pos(H + a, H + b); });
+	else if (which == 1)
+		dsb_msort(idx, tmpi, n, [H](uint32_t a, uint32_t b) -> int { return dsb_chain_cmp_by_MEM_score(H + a, H + b); });
+	else if (which == 2)
+		dsb_msort(idx, tmpi, n, [H](uint32_t a, uint32_t b) -> int { return dsb_chain_cmp_by_score(H + a, H + b); });
+	else if (which == 3) {
+		dsb_anchor_t *A = (dsb_anchor_t *)T; /* n anchors fit: sizeof(anchor) <= sizeof(chain) */
+		for (uint32_t k = 0; k < n; k++) {
+			dsb_anchor_t a;
+			memset(&a, 0, sizeof(a));
+			a.ref_ID = H[k].ref_ID; a.direction = H[k].with_top_anchor; a.ref_offset = H[k].t_st;
+			A[k] = a;
+		}
+		dsb_msort(idx, tmpi, n, [A](uint32_t a, uint32_t b) -> int { return dsb_anchor_cmp(A + a, A + b); });
+	} else {
+		dsb_mem_t *M = (dsb_mem_t *)T;
+		for (uint32_t k = 0; k < n; k++) {
+			dsb_mem_t m;
+			memset(&m, 0, sizeof(m));
+			m.match_len = (int)H[k].sum_score + (int)H[k].t_st;
+			M[k] = m;
+		}
+		dsb_msort(idx, tmpi, n, [M](uint32_t a, uint32_t b) -> int { return dsb_mem_cmp(M + a, M + b); });
+	}
+}
+
+__global__ void k_selftest_sort(dsb_chain_t *chains, dsb_chain_t *tmp, uint32_t *idx, uint32_t *tmpi, uint32_t n,
+				 uint32_t n_arrays, int which)
+{
+	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= n_arrays)
+		return;
+	size_t o = (size_t)t * n;
+	dsb_selftest_one(chains + o, tmp + o, idx + o, tmpi + o, n, which);
+}
+
+/* ------------------------------------------------------------------ host side */
+/* device buffer that grows (persistent per device context; calls are serialised) */
+struct dbuf {
+	void *p = nullptr;
+	size_t cap = 0;
+	int ensure(size_t n, char *err, size_t errn)
+	{
+		if (n <= cap)
+			return 0;
+		if (p)
+			hipFree(p);
+		p = nullptr;
+		cap = 0;
+		size_t c = n + n / 8 + 4096;
+		HIP_OK(hipMalloc(&p, c));
+		cap = c;
+		return 0;
+	}
+	void release()
+	{
+		if (p)
+			hipFree(p);
+		p = nullptr;
+		cap = 0;
+	}
+	template <typename T> T *as() const { return (T *)p; }
+};
+
+struct dsb_gpu_dev {
+	int device;
+	hipStream_t stream;
+	hipEvent_t ev_a, ev_b;
+	pthread_mutex_t mu;
+	dsb_dindex_t h;          /* host copy holding device pointers */
+	dsb_dindex_t *d;         /* device copy */
+	std::vector<void *> allocs;
+	dbuf seq, seq_off, len, ws_off, scale, ws, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2;
+};
+
+template <typename T>
+static int upload(dsb_gpu_dev *g, const T *src, size_t count, const T **dst, char *err, size_t errn)
+{
+	void *p = nullptr;
+	size_t bytes = count * sizeof(T);
+	HIP_OK(hipMalloc(&p, bytes ? bytes : 16));
+	if (bytes)
+		HIP_OK(hipMemcpy(p, src, bytes, hipMemcpyHostToDevice));
+	g->allocs.push_back(p);
+	*dst = (const T *)p;
+	return 0;
+}
+
+extern "C" int dsb_gpu_device_count(void)
+{
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess)
+		return 0;
+	return n;
+}
+
+extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
+{
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+		snprintf(err, errn, "no HIP device visible: the deSAMBA MI355X classify path has no CPU fallback");
+		return -1;
+	}
+	if (device < 0) {
+		const char *e = getenv("DSB_DEVICE");
+		if (e)
+			device = atoi(e);
+		else
+			HIP_OK(hipGetDevice(&device));
+	}
+	if (device >= ndev) {
+		snprintf(err, errn, "device %d out of range (%d visible)", device, ndev);
+		return -1;
+	}
+	HIP_OK(hipSetDevice(device));
+	dsb_gpu_dev *g = new dsb_gpu_dev();
+	g->device = device;
+	pthread_mutex_init(&g->mu, NULL);
+	HIP_OK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+	HIP_OK(hipEventCreate(&g->ev_a));
+	HIP_OK(hipEventCreate(&g->ev_b));
+	dsb_dindex_t &h = g->h;
+	memset(&h, 0, sizeof(h));
+	/* bwt_occ: + 256 B slack (occ reads whole 16-nibble words) */
+	if (upload(g, ix->bwt_occ, ix->byteLen + 256, &h.bwt_occ, err, errn)) return -1;
+	h.byteLen = ix->byteLen;
+	memcpy(h.rank, ix->rank, sizeof(h.rank));
+	if (upload(g, ix->hash_index, (1ull << 26) + 1, &h.hash_index, err, errn)) return -1;
+	if (upload(g, ix->sa, ix->sa_size, &h.sa, err, errn)) return -1;
+	h.sa_size = ix->sa_size;
+	h.dollor_pos = ix->dollor_pos;
+	if (upload(g, ix->ek0, ix->ek_size, &h.ek0, err, errn)) return -1;
+	if (upload(g, ix->ek1, ix->ek_size, &h.ek1, err, errn)) return -1;
+	h.ek_size = ix->ek_size;
+	h.ek_mask = ix->ek_mask;
+	h.l_ek = ix->l_ek;
+	h.single_base_max = ix->single_base_max;
+	if (upload(g, ix->uni, ix->n_uni + 2, &h.uni, err, errn)) return -1;
+	h.n_uni = ix->n_uni;
+	if (upload(g, ix->ref_bin, ix->ref_bin_padded, &h.ref_bin, err, errn)) return -1;
+	h.ref_bin_n = ix->ref_bin_n;
+	h.ref_bin_padded = ix->ref_bin_padded;
+	if (upload(g, ix->ref_seq_offset, ix->n_ref, &h.ref_seq_offset, err, errn)) return -1;
+	if (upload(g, ix->ref_seq_l, ix->n_ref, &h.ref_seq_l, err, errn)) return -1;
+	h.n_ref = ix->n_ref;
+	if (upload(g, ix->r_p, ix->n_rp + 64, &h.r_p, err, errn)) return -1;
+	h.n_rp = ix->n_rp;
+	if (upload(g, ix->Q_MEM, (size_t)DSB_Q_MEM_PAD, &h.Q_MEM, err, errn)) return -1;
+	if (upload(g, ix->Q_LV, (size_t)DSB_LV_DIM * DSB_LV_DIM, &h.Q_LV, err, errn)) return -1;
+	h.filter_min_length = ix->filter_min_length;
+	h.filter_min_score = ix->filter_min_score;
+	h.filter_min_score_LV3 = ix->filter_min_score_LV3;
+	const dsb_dindex_t *dptr;
+	if (upload(g, &h, 1, &dptr, err, errn)) return -1;
+	g->d = (dsb_dindex_t *)dptr;
+	ix->gpu = g;
+	return 0;
+}
+
+extern "C" void dsb_gpu_free(dsb_index *ix)
+{
+	dsb_gpu_dev *g = (dsb_gpu_dev *)ix->gpu;
+	if (!g)
+		return;
+	hipSetDevice(g->device);
+	for (void *p : g->allocs)
+		hipFree(p);
+	dbuf *bs[] = {&g->seq, &g->seq_off, &g->len, &g->ws_off, &g->scale, &g->ws, &g->order, &g->word_off,
+		      &g->ro, &g->mrl, &g->hits, &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2};
+	for (dbuf *b : bs)
+		b->release();
+	hipEventDestroy(g->ev_a);
+	hipEventDestroy(g->ev_b);
+	hipStreamDestroy(g->stream);
+	pthread_mutex_destroy(&g->mu);
+	delete g;
+	ix->gpu = NULL;
+}
+
+static double now_ms(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+}
+
+static float ev_ms(dsb_gpu_dev *g)
+{
+	hipEventRecord(g->ev_b, g->stream);
+	hipEventSynchronize(g->ev_b);
+	float ms = 0;
+	hipEventElapsedTime(&ms, g->ev_a, g->ev_b);
+	return ms;
+}
+
+static size_t ws_budget(void)
+{
+	const char *e = getenv("DSB_WS_BUDGET_MB");
+	if (e)
+		return (size_t)atoll(e) << 20;
+	size_t fr = 0, tot = 0;
+	if (hipMemGetInfo(&fr, &tot) != hipSuccess)
+		return (size_t)8 << 30;
+	size_t b = fr / 2;
+	size_t cap = (size_t)48 << 30;
+	return b < cap ? b : cap;
+}
+
+/* seed-wave prefix over a read list: 2 strands x ceil(lk/64) words for reads >= 40 bp */
+static uint64_t seed_words(const std::vector<uint32_t> &len, uint64_t cb, const uint32_t *sel, size_t m, int l_ek,
+			   std::vector<uint64_t> &off, uint64_t *positions)
+{
+	off.resize(m + 1);
+	uint64_t tw = 0;
+	for (size_t i = 0; i < m; i++) {
+		off[i] = tw;
+		uint32_t L = len[cb + (sel ? sel[i] : i)];
+		if (L >= DSB_MIN_READ_LEN) {
+			uint32_t lk = L - l_ek + 1;
+			tw += 2ull * ((lk + 63) / 64);
+			if (positions)
+				*positions += 2ull * lk;
+		}
+	}
+	off[m] = tw;
+	return tw;
+}
+
+static int classify_locked(dsb_gpu_dev *g, dsb_index *ix, const dsb_reads_t *reads, int *max_read_l,
+			   dsb_read_out_t *ro, std::vector<dsb_hit_out_t> &hv, int stats_on, dsb_gpu_timing &T, char *err,
+			   size_t errn)
+{
+	HIP_OK(hipSetDevice(g->device));
+	hipStream_t s = g->stream;
+	uint64_t n = reads->n;
+	/* ---- reads: bases only, concatenated */
+	std::vector<uint64_t> seq_off(n);
+	std::vector<uint32_t> len(n);
+	uint64_t tot = 0;
+	for (uint64_t i = 0; i < n; i++) {
+		seq_off[i] = tot;
+		len[i] = reads->rec[i].seq_l;
+		tot += len[i];
+	}
+	T.n_bases = tot;
+	if (n == 0)
+		return 0;
+	if (g->seq.ensure(tot + 16, err, errn) || g->seq_off.ensure(8 * n + 8, err, errn) ||
+	    g->len.ensure(4 * n + 4, err, errn) || g->scale.ensure(4 * n + 4, err, errn) ||
+	    g->ro.ensure(sizeof(dsb_read_out_t) * n + 64, err, errn) || g->mrl.ensure(4 * n + 4, err, errn) ||
+	    g->hit_off.ensure(4 * n + 4, err, errn) || g->cnt.ensure(64, err, errn) || g->stats.ensure(8 * 16, err, errn) ||
+	    g->ws_off.ensure(8 * n + 8, err, errn))
+		return -1;
+	double th = now_ms();
+	{
+		std::vector<uint8_t> stage(tot + 16); /* pack sequences (the arena also holds names/quals) */
+		for (uint64_t i = 0; i < n; i++)
+			memcpy(stage.data() + seq_off[i], reads->arena + reads->rec[i].seq_off, len[i]);
+		HIP_OK(hipMemcpyAsync(g->seq.p, stage.data(), tot, hipMemcpyHostToDevice, s));
+		HIP_OK(hipMemcpyAsync(g->seq_off.p, seq_off.data(), 8 * n, hipMemcpyHostToDevice, s));
+		HIP_OK(hipMemcpyAsync(g->len.p, len.data(), 4 * n, hipMemcpyHostToDevice, s));
+		HIP_OK(hipStreamSynchronize(s));
+	}
+	T.ms_h2d += now_ms() - th;
+	HIP_OK(hipMemsetAsync(g->stats.p, 0, 8 * 16, s));
+	std::vector<uint32_t> scale(n, 1);
+	std::vector<uint64_t> ws_off(n);
+	std::vector<dsb_read_out_t> h_ro(n);
+	std::vector<int32_t> mrl(n);
+	std::vector<uint32_t> hit_off(n);
+	std::vector<uint64_t> word_off;
+	size_t budget = ws_budget();
+	int carry = *max_read_l;
+	int l_ek = ix->l_ek;
+	for (uint64_t cb = 0; cb < n;) {
+		/* ---- chunk [cb, ce) within the workspace budget, input order */
+		uint64_t ce = cb, ws_total = 0;
+		while (ce < n) {
+			uint64_t sz = dsb_layout(len[ce], dsb_default_caps(len[ce], 1)).total;
+			if (ce > cb && ws_total + sz > budget)
+				break;
+			ws_off[ce] = ws_total;
+			ws_total += sz;
+			ce++;
+		}
+		uint32_t cn = (uint32_t)(ce - cb);
+		T.n_chunks++;
+		if (g->ws.ensure(ws_total + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
+		    g->word_off.ensure(8 * (size_t)cn + 16, err, errn))
+			return -1;
+		HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
+		HIP_OK(hipMemcpyAsync(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
+		const uint32_t *cl = g->len.as<uint32_t>() + cb;
+		const uint64_t *cso = g->seq_off.as<uint64_t>() + cb;
+		/* length-sorted order (longest first) for the one-lane-per-read kernels */
+		std::vector<uint32_t> order(cn);
+		for (uint32_t i = 0; i < cn; i++) order[i] = i;
+		std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return len[cb + a] > len[cb + b]; });
+		HIP_OK(hipMemcpyAsync(g->order.p, order.data(), 4ull * cn, hipMemcpyHostToDevice, s));
+		uint64_t tw = seed_words(len, cb, nullptr, cn, l_ek, word_off, &T.seed_positions);
+		HIP_OK(hipMemcpyAsync(g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
+		uint8_t *wsb = g->ws.as<uint8_t>();
+		hipEventRecord(g->ev_a, s);
+		k_encode<<<cn, 256, 0, s>>>(g->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, nullptr, cn);
+		T.ms_encode += ev_ms(g);
+		HIP_OK(hipGetLastError());
+		if (tw) {
+			hipEventRecord(g->ev_a, s);
+			k_seed<<<(uint32_t)((tw * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
+										     g->word_off.as<uint64_t>(), nullptr, cn, tw);
+			T.ms_seed += ev_ms(g);
+			HIP_OK(hipGetLastError());
+		}
+		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
+		hipEventRecord(g->ev_a, s);
+		if (stats_on)
+			k_classA<true><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
+								     g->order.as<uint32_t>(), cn, g->ro.as<dsb_read_out_t>(),
+								     g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>());
+		else
+			k_classA<false><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
+								      g->order.as<uint32_t>(), cn, g->ro.as<dsb_read_out_t>(),
+								      g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>());
+		T.ms_classA += ev_ms(g);
+		HIP_OK(hipGetLastError());
+		uint32_t n_over = 0;
+		HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
+		HIP_OK(hipMemcpy(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
+		/* ---- overflow: re-run those reads with 8x capacities in extra workspace */
+		while (n_over) {
+			std::vector<uint32_t> sel;
+			for (uint32_t i = 0; i < cn; i++)
+				if (h_ro[cb + i].status) sel.push_back(i);
+			T.n_retry += sel.size();
+			uint64_t tot2 = 0;
+			for (uint32_t i : sel) {
+				scale[cb + i] *= DSB_CAP_RETRY;
+				if (scale[cb + i] > 4096) {
+					snprintf(err, errn, "read %lu overflows every workspace size", (unsigned long)(cb + i));
+					return -1;
+				}
+				ws_off[cb + i] = ws_total + tot2;
+				tot2 += dsb_layout(len[cb + i], dsb_default_caps(len[cb + i], scale[cb + i])).total;
+			}
+			{ /* grow the chunk workspace, keeping the first ws_total bytes */
+				void *np = nullptr;
+				size_t need = ws_total + tot2 + 4096;
+				HIP_OK(hipMalloc(&np, need));
+				HIP_OK(hipMemcpyAsync(np, g->ws.p, ws_total, hipMemcpyDeviceToDevice, s));
+				HIP_OK(hipStreamSynchronize(s));
+				hipFree(g->ws.p);
+				g->ws.p = np;
+				g->ws.cap = need;
+				ws_total += tot2;
+				wsb = g->ws.as<uint8_t>();
+			}
+			HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
+			HIP_OK(hipMemcpyAsync(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
+			std::vector<uint64_t> wo2;
+			uint64_t tw2 = seed_words(len, cb, sel.data(), sel.size(), l_ek, wo2, nullptr);
+			if (g->sel.ensure(4 * sel.size() + 4, err, errn) || g->wo2.ensure(8 * wo2.size() + 16, err, errn))
+				return -1;
+			HIP_OK(hipMemcpyAsync(g->sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(hipMemcpyAsync(g->wo2.p, wo2.data(), 8 * wo2.size(), hipMemcpyHostToDevice, s));
+			uint32_t m = (uint32_t)sel.size();
+			k_encode<<<m, 256, 0, s>>>(g->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, g->sel.as<uint32_t>(), m);
+			if (tw2)
+				k_seed<<<(uint32_t)((tw2 * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
+											      g->wo2.as<uint64_t>(), g->sel.as<uint32_t>(), m, tw2);
+			HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
+			k_classA<false><<<(m + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
+								     g->sel.as<uint32_t>(), m, g->ro.as<dsb_read_out_t>(),
+								     g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>());
+			HIP_OK(hipGetLastError());
+			HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
+			HIP_OK(hipMemcpy(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
+		}
+		if (getenv("DSB_DEBUG_READ")) { /* diagnostic: dump one read's workspace after stage A */
+			uint64_t dr = strtoull(getenv("DSB_DEBUG_READ"), NULL, 10);
+			if (dr >= cb && dr < ce) {
+				uint32_t i = (uint32_t)(dr - cb);
+				dsb_ws_layout lay = dsb_layout(len[dr], dsb_default_caps(len[dr], scale[dr]));
+				std::vector<uint8_t> hbuf(lay.total);
+				HIP_OK(hipMemcpy(hbuf.data(), wsb + ws_off[dr], lay.total, hipMemcpyDeviceToHost));
+				dsb_read_ws w;
+				dsb_ws_init(&w, &g->h, hbuf.data(), len[dr], dsb_default_caps(len[dr], scale[dr]));
+				w.n_anc = h_ro[dr].n_anchor; w.n_hit = h_ro[dr].n_hit; w.fast_classify = h_ro[dr].fast;
+				w.overflow = h_ro[dr].status; w.reached_update = h_ro[dr].reached_update;
+				(void)i;
+				const dsb_sdir_t *sv = (const dsb_sdir_t *)(hbuf.data() + lay.state);
+				w.sd[0] = sv[0];
+				w.sd[1] = sv[1];
+				dsb_debug_dump(stderr, &w, "gpuA");
+			}
+		}
+		/* ---- max_read_l carry (src/cly.c:2953): prefix max over reads reaching the update */
+		uint64_t worst = 0;
+		for (uint32_t i = 0; i < cn; i++) {
+			if (h_ro[cb + i].reached_update && (int)len[cb + i] > carry)
+				carry = (int)len[cb + i];
+			mrl[cb + i] = carry;
+			worst += h_ro[cb + i].n_hit;
+		}
+		HIP_OK(hipMemcpyAsync(g->mrl.p, mrl.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
+		if (g->hits.ensure(sizeof(dsb_hit_out_t) * worst + 4096, err, errn))
+			return -1;
+		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
+		hipEventRecord(g->ev_a, s);
+		k_classB<<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
+							 g->order.as<uint32_t>(), cn, g->mrl.as<int32_t>(), g->ro.as<dsb_read_out_t>(),
+							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>());
+		T.ms_classB += ev_ms(g);
+		HIP_OK(hipGetLastError());
+		double td = now_ms();
+		uint32_t nh = 0;
+		HIP_OK(hipMemcpy(&nh, g->cnt.p, 4, hipMemcpyDeviceToHost));
+		HIP_OK(hipMemcpy(ro + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
+		HIP_OK(hipMemcpy(hit_off.data() + cb, g->hit_off.p, 4ull * cn, hipMemcpyDeviceToHost));
+		uint64_t base = hv.size();
+		hv.resize(base + nh);
+		if (nh)
+			HIP_OK(hipMemcpy(hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost));
+		for (uint32_t i = 0; i < cn; i++)
+			ro[cb + i].hit_off = base + hit_off[cb + i];
+		T.ms_d2h += now_ms() - td;
+		cb = ce;
+	}
+	*max_read_l = carry;
+	if (stats_on) {
+		unsigned long long st[16];
+		HIP_OK(hipMemcpy(st, g->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+		for (int k = 0; k < 16; k++) T.stats[k] = st[k];
+	}
+	return 0;
+}
+
+extern "C" int dsb_gpu_classify(dsb_index *ix, const dsb_reads_t *reads, int *max_read_l, dsb_read_out_t *ro,
+				dsb_hit_out_t **hits, uint64_t *n_hits, int stats_on, dsb_gpu_timing *tm, char *err,
+				size_t errn)
+{
+	dsb_gpu_dev *g = (dsb_gpu_dev *)ix->gpu;
+	if (!g) {
+		snprintf(err, errn, "index not resident on a GPU (dsb_gpu_init not called)");
+		return -1;
+	}
+	double t0 = now_ms();
+	dsb_gpu_timing T;
+	memset(&T, 0, sizeof(T));
+	T.n_reads = reads->n;
+	pthread_mutex_lock(&g->mu);
+	std::vector<dsb_hit_out_t> hv;
+	int rc = classify_locked(g, ix, reads, max_read_l, ro, hv, stats_on, T, err, errn);
+	pthread_mutex_unlock(&g->mu);
+	*n_hits = hv.size();
+	*hits = (dsb_hit_out_t *)malloc(sizeof(dsb_hit_out_t) * (hv.size() + 1));
+	if (*hits && !hv.empty())
+		memcpy(*hits, hv.data(), sizeof(dsb_hit_out_t) * hv.size());
+	T.ms_total = now_ms() - t0;
+	if (tm)
+		*tm = T;
+	return rc;
+}
+
+/* GPU self-test of the glibc-msort restatement: n_arrays x n random keys sorted on the device
+ * and on the host with the same code; returns the number of arrays whose permutation differs. */
+extern "C" int dsb_gpu_selftest_sort(uint32_t n, uint32_t n_arrays, int which, uint32_t seed)
+{
+	char err[256];
+	size_t errn = sizeof(err);
+	size_t tot = (size_t)n * n_arrays;
+	std::vector<dsb_chain_t> h(tot), tmp(tot);
+	std::vector<uint32_t> hi(tot), ht(tot), back(tot);
+	uint32_t x = seed | 1;
+	auto rnd = [&]() { x ^= x << 13; x ^= x >> 17; x ^= x << 5; return x; };
+	for (auto &c : h) {
+		memset(&c, 0, sizeof(c));
+		c.ref_ID = rnd() % 4;
+		c.t_st = rnd() % 8;
+		c.sum_score = rnd() % 6;
+		c.q_st = rnd() % 100;
+		c.q_ed = c.q_st + rnd() % 100;
+		c.with_top_anchor = rnd() & 1;
+		c.indel = rnd() % 3;
+	}
+	dsb_chain_t *dc, *dt;
+	uint32_t *di, *dti;
+	HIP_OK(hipMalloc(&dc, tot * sizeof(dsb_chain_t)));
+	HIP_OK(hipMalloc(&dt, tot * sizeof(dsb_chain_t)));
+	HIP_OK(hipMalloc(&di, tot * 4));
+	HIP_OK(hipMalloc(&dti, tot * 4));
+	HIP_OK(hipMemcpy(dc, h.data(), tot * sizeof(dsb_chain_t), hipMemcpyHostToDevice));
+	k_selftest_sort<<<(n_arrays + 63) / 64, 64>>>(dc, dt, di, dti, n, n_arrays, which);
+	HIP_OK(hipDeviceSynchronize());
+	HIP_OK(hipMemcpy(back.data(), di, tot * 4, hipMemcpyDeviceToHost));
+	(void)hipFree(dc); (void)hipFree(dt); (void)hipFree(di); (void)hipFree(dti);
+	int bad = 0;
+	for (uint32_t a = 0; a < n_arrays; a++) {
+		size_t o = (size_t)a * n;
+		dsb_selftest_one(h.data() + o, tmp.data() + o, hi.data() + o, ht.data() + o, n, which);
+		if (memcmp(hi.data() + o, back.data() + o, 4ull * n) != 0)
+			bad++;
+	}
+	return bad;
+}

@@ -1,0 +1,112 @@
+"""ctypes binding of lib/libdesamba.so for tests and bench.py.
+
+Mirrors the reference's three ABI calls (include/desamba.h) plus the extension entry
+points of include/desamba_mi355x.h.  The library is built in-tree by `make -C
+desamba-so_amd`; there is no Python or CPU fallback for classification.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libdesamba.so")
+
+FMT_SAM, FMT_SAM_FULL, FMT_DES, FMT_DES_FULL = 1, 2, 3, 4
+ST_NAMES = ["occ", "occ_nib", "mem_search", "sa", "uni", "ref_pos", "getref_b", "anchor", "chain", "ek1", "ek2"]
+
+
+class Timing(C.Structure):
+    _fields_ = [("stats_on", C.c_int), ("pad", C.c_int), ("ms_total", C.c_double), ("ms_h2d", C.c_double),
+                ("ms_d2h", C.c_double), ("ms_encode", C.c_double), ("ms_seed", C.c_double),
+                ("ms_classA", C.c_double), ("ms_classB", C.c_double), ("n_reads", C.c_uint64),
+                ("n_bases", C.c_uint64), ("n_retry", C.c_uint64), ("n_chunks", C.c_uint64),
+                ("seed_positions", C.c_uint64), ("stats", C.c_uint64 * 16)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("stats", "pad")}
+        d["stats"] = {n: int(self.stats[i]) for i, n in enumerate(ST_NAMES)}
+        return d
+
+
+_lib = None
+
+
+def lib(path: str | None = None):
+    """Load the shared library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or os.environ.get("DSB_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise RuntimeError(f"{p} not built: run `make -C desamba-so_amd` (hipcc, gfx950)")
+    L = C.CDLL(p, mode=C.RTLD_GLOBAL)
+    vp, pp, u64, u64p = C.c_void_p, C.POINTER(C.c_char_p), C.c_uint64, C.POINTER(C.c_uint64)
+    L.load_index.argtypes = [C.POINTER(vp), C.c_char_p]
+    L.load_index.restype = None
+    L.read_classify.argtypes = [vp, C.c_char_p, u64, C.POINTER(C.c_void_p), u64p, C.c_int, C.c_int]
+    L.read_classify.restype = None
+    L.meta_analysis.argtypes = [vp, C.c_char_p, u64, C.POINTER(C.c_void_p), u64p, C.c_int, C.c_int, u64,
+                                C.POINTER(C.c_void_p), u64p]
+    L.meta_analysis.restype = None
+    L.dsb_classify_text.argtypes = [vp, C.c_char_p, u64, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_void_p), u64p,
+                                    C.POINTER(Timing)]
+    L.dsb_classify_text.restype = C.c_int
+    L.dsb_version.restype = C.c_char_p
+    L.dsb_device_count.restype = C.c_int
+    L.dsb_free.argtypes = [vp]
+    L.dsb_unload_index.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def _take(L, p: C.c_void_p, n: int) -> bytes:
+    if not p.value:
+        return b""
+    b = C.string_at(p.value, n)
+    L.dsb_free(p)
+    return b
+
+
+class Index:
+    """An index resident in the HBM of one GPU (reference load_index)."""
+
+    def __init__(self, dirpath: str):
+        self.L = lib()
+        h = C.c_void_p()
+        self.L.load_index(C.byref(h), dirpath.encode())
+        self.h = h
+
+    def read_classify(self, data: bytes | str, thread_id: int = 0, thread_num: int = 1) -> bytes:
+        """data: FASTQ/FASTA bytes, or a path (str) -> input_n = (uint64_t)-1."""
+        out, n = C.c_void_p(), C.c_uint64(0)
+        if isinstance(data, str):
+            self.L.read_classify(self.h, data.encode(), C.c_uint64(0xFFFFFFFFFFFFFFFF), C.byref(out), C.byref(n),
+                                 thread_id, thread_num)
+        else:
+            self.L.read_classify(self.h, data, len(data), C.byref(out), C.byref(n), thread_id, thread_num)
+        return _take(self.L, out, n.value)
+
+    def classify(self, data: bytes, fmt: int = FMT_SAM_FULL, max_read_l: int = 0, stats: bool = False):
+        """-> (output bytes, timing dict, carried max_read_l)"""
+        out, n = C.c_void_p(), C.c_uint64(0)
+        mrl = C.c_int(max_read_l)
+        t = Timing()
+        t.stats_on = 1 if stats else 0
+        rc = self.L.dsb_classify_text(self.h, data, len(data), fmt, C.byref(mrl), C.byref(out), C.byref(n),
+                                      C.byref(t))
+        if rc != 0:
+            raise RuntimeError("dsb_classify_text failed")
+        return _take(self.L, out, n.value), t.as_dict(), mrl.value
+
+    def meta_analysis(self, sam: bytes, flag: int = 0, max_snapshot_len: int = 65536, thread_id: int = 0):
+        out, n = C.c_void_p(), C.c_uint64(0)
+        snap, sn = C.c_void_p(), C.c_uint64(0)
+        self.L.meta_analysis(self.h, sam, len(sam), C.byref(out), C.byref(n), thread_id, flag, max_snapshot_len,
+                             C.byref(snap), C.byref(sn))
+        return _take(self.L, out, n.value), _take(self.L, snap, sn.value)
+
+    def close(self):
+        if self.h:
+            self.L.dsb_unload_index(self.h)
+            self.h = None

@@ -19,6 +19,7 @@
  *                (default on in the herm_classify build).
  *   --dump F     per-read stage dump (seeds, anchors, chains) to file F.
  *   --max-read-l N  initial max_read_l carried into the first read.
+ *   --sam        SAM instead of SAM_FULL (SEQ and QUAL printed as '*').
  *
  * usage: ref_classify [opts] <index_dir> <reads.fq>
  */
@@ -160,7 +161,7 @@ static void pool_free(Classify_buff_pool *b)
 int main(int argc, char **argv)
 {
 	int fresh = HERMETIC_DEFAULT, perturb = HERMETIC_DEFAULT;
-	int max_read_l = 0;
+	int max_read_l = 0, with_seq = 1;
 	const char *dump_path = NULL;
 	int ai = 1;
 	for (; ai < argc && argv[ai][0] == '-' && argv[ai][1] == '-'; ai++) {
@@ -170,6 +171,7 @@ int main(int argc, char **argv)
 		else if (!strcmp(argv[ai], "--no-perturb")) perturb = 0;
 		else if (!strcmp(argv[ai], "--dump") && ai + 1 < argc) dump_path = argv[++ai];
 		else if (!strcmp(argv[ai], "--max-read-l") && ai + 1 < argc) max_read_l = atoi(argv[++ai]);
+		else if (!strcmp(argv[ai], "--sam")) with_seq = 0; /* SAM: SEQ/QUAL printed as '*' */
 		else { fprintf(stderr, "unknown option %s\n", argv[ai]); return 2; }
 	}
 	if (ai + 2 > argc) {
@@ -238,12 +240,12 @@ int main(int argc, char **argv)
 				b.max_read_l = max_read_l;
 				classify_one(seq, idx, &r, &b);
 				max_read_l = b.max_read_l;
-				output_one_result_sam(idx, &r, 1, &o);
+				output_one_result_sam(idx, &r, with_seq, &o);
 				free(r.hit.a); free(r.anchor_v.a);
 				pool_free(&b);
 			} else {
 				classify_one(seq, idx, shared_r + i, &shared);
-				output_one_result_sam(idx, shared_r + i, 1, &o);
+				output_one_result_sam(idx, shared_r + i, with_seq, &o);
 			}
 			n++;
 		}

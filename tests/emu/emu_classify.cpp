@@ -17,6 +17,7 @@ extern "C" {
 #include "../../desamba-so_amd/csrc/dsb_host.h"
 }
 #include "../../desamba-so_amd/csrc/gpu/dsb_ws.h"
+#include "../../desamba-so_amd/csrc/gpu/dsb_debug.h"
 
 int main(int argc, char **argv)
 {
@@ -68,7 +69,7 @@ int main(int argc, char **argv)
 		for (uint32_t scale = 1;; scale *= DSB_CAP_RETRY) {
 			dsb_caps_t cap = dsb_default_caps(L, scale);
 			dsb_ws_layout lay = dsb_layout(L, cap);
-			arena.assign(lay.total + 256, 0xEE);
+			arena.assign(lay.total + 256, (uint8_t)(getenv("EMU_FILL") ? strtol(getenv("EMU_FILL"), 0, 0) : 0xEE));
 			dsb_read_ws w;
 			dsb_ws_init(&w, &d, arena.data(), L, cap);
 			if (stats) w.stats = st;
@@ -89,6 +90,8 @@ int main(int argc, char **argv)
 				}
 			}
 			dsb_classify_A(&w);
+			if (getenv("DSB_DEBUG_READ") && strtoull(getenv("DSB_DEBUG_READ"), 0, 10) == i)
+				dsb_debug_dump(stderr, &w, "emuA");
 			if (w.overflow) {
 				n_retry++;
 				continue;

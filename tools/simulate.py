@@ -199,7 +199,8 @@ def simulate_reads(genomes, n_reads, seed, kind="ont", mean_len=8000, sigma=0.5,
                 strand = "-"
             name = f"rd{i}_{src[gi]['taxid']}_{p}_{strand}_{int(err * 100)}"
         s = BASES[seq].tobytes()
-        q = (rng.integers(33 + 5, 33 + 40, size=len(s), dtype=np.uint8)).tobytes()
+        # low-entropy qualities (one symbol per read) keep committed fixtures small
+        q = bytes([33 + 10 + (i % 30)]) * len(s)
         yield name, s, q
 
 
@@ -304,6 +305,29 @@ def read_fasta_genomes(path):
     if name is not None:
         genomes.append(_mk(name, buf, lut))
     return genomes
+
+
+def read_fasta_genomes_from_index(idx_dir):
+    """Genomes decoded from an index's packed reference (deSAMBA.ref_b / .ref_i, idx.c:1141-1152),
+    so reads can be simulated where only the index exists (e.g. the GPU box)."""
+    import numpy as np
+    with open(os.path.join(idx_dir, "deSAMBA.ref_i"), "rb") as f:
+        n = struct.unpack("<Q", f.read(8))[0]
+        infos = []
+        for _ in range(n):
+            rec = f.read(144)
+            name = rec[:128].split(b"\0", 1)[0].decode()
+            seq_l, seq_off = struct.unpack("<QQ", rec[128:144])
+            infos.append((name, seq_l, seq_off))
+    packed = np.fromfile(os.path.join(idx_dir, "deSAMBA.ref_b"), dtype=np.uint8, offset=8)
+    bases = np.empty(len(packed) * 4, dtype=np.uint8)
+    for k in range(4):
+        bases[k::4] = (packed >> (6 - 2 * k)) & 3
+    out = []
+    for name, seq_l, seq_off in infos:
+        taxid = int(name.split("|")[1]) if name.startswith("tid|") else 0
+        out.append(dict(name=name, taxid=taxid, seq=bases[seq_off:seq_off + seq_l].copy(), decoy="DECOY" in name))
+    return out
 
 
 def _mk(name, buf, lut):
