@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X classify path (BASELINE.json metric, config C1).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--index DIR]
+
+A step = classify one batch of R synthetic ONT reads (lognormal, mean 8 kb, 5-15 % error)
+already resident in HBM (dsb_batch_run: seed + occ/rank + chaining + scoring on the GPU,
+results back on the host), then assign one taxon per read exactly as meta_analysis does
+(reference src/cly_mt.c:902-961) and reduce the per-taxon counts across ranks with RCCL
+(all_reduce over torch.distributed "nccl" when N > 1).  Reads shard across ranks (weak
+scaling: every rank classifies its own R reads); the index is replicated in each GPU's HBM.
+
+Workload C1: the >=50 Mbp synthetic family-structured proxy index (data/c1_index.txz,
+made by tools/make_c1_index.sh with the reference's own index builder; the demo human
+index is not available offline) + R = 100k reads per rank.  If data/c1_index.txz is
+absent the committed fixture index is used and config.workload says so.
+
+The JSON line carries:
+  roofline     k_classA (the dominant kernel): algorithmic bytes per launch from the work
+               counters of one untimed stats run / its average launch
+               time from HIP events on the library's stream over the timed steps;
+               traffic = HBM bytes per launch from the committed PMC profile of this
+               workload (profiles/), or null.
+  cpu_baseline the reference classifier (oracle/_ref/deSAMBA, built from the reference
+               sources by oracle/Makefile) on the host cores, on a bounded sample of the
+               same reads; rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import re
+import subprocess
+import sys
+import tarfile
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "desamba-so_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+METRIC = "long reads classified/sec + Gbases/sec at 1/2/4/8 MI355X; bit-exact taxid match"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+ST = ["occ", "occ_nib", "mem_search", "sa", "uni", "ref_pos", "getref_b", "anchor", "chain", "ek1", "ek2"]
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+# ----------------------------------------------------------------------------- inputs
+def _tmp():
+    return os.environ.get("TMPDIR", "/tmp")
+
+
+def unpack_index(rank: int) -> tuple[str, str]:
+    """-> (index dir, workload name).  Rank 0 unpacks, the others wait for it."""
+    txz = os.path.join(ROOT, "data", "c1_index.txz")
+    if os.path.exists(txz):
+        name, src = "C1-proxy-56Mbp", txz
+    else:
+        name, src = "C0-fixture-1Mbp", os.path.join(ROOT, "tests", "golden", "fixture_index.txz")
+    st = os.stat(src)
+    key = hashlib.sha1(f"{src}:{st.st_size}:{int(st.st_mtime)}".encode()).hexdigest()[:12]
+    d = os.path.join(_tmp(), f"dsb_index_{key}")
+    done = os.path.join(d, ".done")
+    if rank == 0 and not os.path.exists(done):
+        tmpd = tempfile.mkdtemp(dir=_tmp(), prefix="dsb_index_part_")
+        t = time.time()
+        with tarfile.open(src) as tf:
+            tf.extractall(tmpd)
+        sub = [e for e in os.listdir(tmpd) if os.path.isdir(os.path.join(tmpd, e))]
+        inner = os.path.join(tmpd, sub[0]) if len(sub) == 1 and not os.path.exists(
+            os.path.join(tmpd, "deSAMBA.bwt")) else tmpd
+        if os.path.exists(d):
+            subprocess.run(["rm", "-rf", d], check=True)
+        os.rename(inner, d)
+        open(done, "w").close()
+        log(f"unpacked {os.path.basename(src)} in {time.time() - t:.1f}s -> {d}")
+    t0 = time.time()
+    while not os.path.exists(done):
+        if time.time() - t0 > 900:
+            raise RuntimeError("timed out waiting for rank 0 to unpack the index")
+        time.sleep(1)
+    return d, name
+
+
+def make_reads(index_dir: str, n: int, seed: int, mean_len: int) -> bytes:
+    """Synthetic ONT reads sampled from the index's own reference (tools/simulate.py)."""
+    path = os.path.join(_tmp(), f"dsb_reads_{os.path.basename(index_dir)}_{n}_{seed}_{mean_len}.fq")
+    if not os.path.exists(path):
+        import simulate
+        t = time.time()
+        genomes = simulate.read_fasta_genomes_from_index(index_dir)
+        part = path + f".part{os.getpid()}"
+        simulate.write_fastq(simulate.simulate_reads(genomes, n, seed, "ont", mean_len), part)
+        os.rename(part, path)
+        log(f"simulated {n} reads (seed {seed}) in {time.time() - t:.1f}s")
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def fastq_head(fq: bytes, n: int) -> bytes:
+    pos = 0
+    for _ in range(4 * n):
+        pos = fq.find(b"\n", pos) + 1
+        if pos == 0:
+            return fq
+    return fq[:pos]
+
+
+# ----------------------------------------------------------------------------- baseline
+def cpu_baseline(index_dir: str, fq: bytes, n_sample: int, threads: int):
+    """The reference CLI (oracle/_ref/deSAMBA, gcc -O3 build of the reference sources) on
+    the first n_sample reads; its own 'N sequences processed in T s' timer (starts after
+    the index load, reference src/cly_mt.c:527,557)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "deSAMBA")
+    if not os.path.exists(exe):
+        return None
+    sample = fastq_head(fq, n_sample)
+    nb = sum(len(l) for i, l in enumerate(sample.split(b"\n")) if i % 4 == 1)
+    with tempfile.TemporaryDirectory(dir=_tmp()) as d:
+        p = os.path.join(d, "sample.fq")
+        with open(p, "wb") as f:
+            f.write(sample)
+        t = time.time()
+        r = subprocess.run([exe, "classify", "-t", str(threads), "-o", os.path.join(d, "o.sam"), index_dir, p],
+                           capture_output=True, text=True, timeout=600)
+        wall = time.time() - t
+    m = re.search(r"(\d+) sequences processed in ([0-9.]+)s", r.stdout + r.stderr)
+    if r.returncode != 0 or not m:
+        log("reference CPU run failed:", r.returncode, (r.stdout + r.stderr)[-400:])
+        return None
+    n, secs = int(m.group(1)), float(m.group(2))
+    return {"value": round(n / secs, 1), "unit": "reads/s", "cores": threads, "kind": "reference",
+            "gbases_per_s": round(nb / secs / 1e9, 5),
+            "sample": f"first {n} reads ({nb / 1e6:.1f} Mbp) of rank 0's batch, `deSAMBA classify -t {threads}` "
+                      f"(gcc -O3 build of the reference sources), own timer {secs:.2f}s, wall {wall:.1f}s incl. index load"}
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reads", type=int, default=100000, help="reads per rank")
+    ap.add_argument("--mean-len", type=int, default=8000)
+    ap.add_argument("--index", default=None, help="index directory (default: C1 proxy)")
+    ap.add_argument("--cpu-sample", type=int, default=16000, help="reads in the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-stats", action="store_true", help="skip the work-counter run (roofline)")
+    a = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ["DSB_DEVICE"] = str(local)
+    import torch
+    assert torch.cuda.is_available(), "bench.py needs an MI355X"
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import pydesamba
+    import shard
+
+    if a.index:
+        index_dir, workload = a.index, os.path.basename(os.path.normpath(a.index))
+    else:
+        index_dir, workload = unpack_index(rank)
+    fq = make_reads(index_dir, a.reads, 1000 + rank, a.mean_len)
+    if dist:
+        dist.barrier()
+    t = time.time()
+    idx = pydesamba.Index(index_dir)
+    log(f"rank {rank}: index resident on cuda:{local} in {time.time() - t:.1f}s")
+    batch = idx.batch(fq)
+    log(f"rank {rank}: {batch.n_reads} reads / {batch.n_bases / 1e6:.1f} Mbp resident in HBM "
+        f"(parse+upload {batch.upload['ms_h2d']:.0f} ms)")
+    n_tax = idx.max_tid() + 1
+    counts = torch.zeros(n_tax, dtype=torch.int64, device="cuda")
+
+    def step():
+        tm = batch.run(max_read_l=0)
+        tid, _ = batch.taxa(0)
+        counts.copy_(shard.reduce_counts(shard.taxon_counts(tid, None, n_tax), "cuda"))
+        return tm
+
+    for _ in range(a.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tms = [step() for _ in range(a.steps)]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    reads_total = batch.n_reads * world * a.steps
+    bases_total = batch.n_bases * world * a.steps
+    classified = int(counts[1:].sum().item())
+
+    # ---- roofline of k_classA: algorithmic bytes (stats run) / avg HIP-event launch time
+    ms_A = sum(t["ms_classA"] for t in tms) / a.steps
+    launches_A = tms[0]["n_chunks"]
+    roof = None
+    stats = None
+    if not a.no_stats:
+        ts = batch.run(max_read_l=0, stats=True)
+        sA = ts["stats"]
+        bytes_A = (batch.n_bases + sA["occ_nib"] + 16 * sA["mem_search"] + 8 * (sA["sa"] + sA["uni"] + sA["ref_pos"])
+                   + sA["getref_b"] + 56 * (sA["anchor"] + sA["chain"]))
+        per_launch = bytes_A / launches_A
+        achieved = per_launch / (ms_A / launches_A / 1e3) / 1e9
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                tj = json.load(f)
+            if tj.get("workload") == workload and tj.get("reads") == a.reads:
+                traffic = tj.get("k_classA_hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "kernel": "k_classA",
+                "algorithmic_bytes_per_launch": int(per_launch), "launches_per_step": launches_A,
+                "avg_launch_ms": round(ms_A / launches_A, 3)}
+        stats = {"A": sA, "B": ts["stats_B"]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(index_dir, fq, min(a.cpu_sample, batch.n_reads), a.cpu_threads)
+
+    if rank == 0:
+        value = reads_total / elapsed
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic ONT reads (tools/simulate.py, lognormal mean 8 kb, 5-15% error) from a synthetic reference",
+            "config": {"workload": workload, "reads_per_rank": batch.n_reads, "mbases_per_rank": round(batch.n_bases / 1e6, 2),
+                       "mean_len": a.mean_len, "parallelism": f"reads sharded over {world} GPU(s), index replicated",
+                       "taxon_reduce": "all_reduce(nccl)" if world > 1 else "none"},
+            "gbases_per_s": round(bases_total / elapsed / 1e9, 4),
+            "classified_reads": classified,
+            "phase_ms": {k: round(sum(t[k] for t in tms) / a.steps, 2)
+                         for k in ("ms_encode", "ms_seed", "ms_classA", "ms_classB", "ms_d2h", "ms_total")},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            line["vs_cpu_baseline"] = round(value / cpu["value"], 2)
+        if stats:
+            line["work_counters"] = stats
+        print(json.dumps(line), flush=True)
+    batch.close()
+    idx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

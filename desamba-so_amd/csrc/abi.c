@@ -123,7 +123,7 @@ int dsb_classify_text(void *idx, const char *text, uint64_t text_n, int format, 
 		timing->n_retry = gt.n_retry;
 		timing->n_chunks = gt.n_chunks;
 		timing->seed_positions = gt.seed_positions;
-		for (int k = 0; k < 16; k++) timing->stats[k] = gt.stats[k];
+		for (int k = 0; k < 32; k++) timing->stats[k] = gt.stats[k];
 	}
 	free(ro);
 	free(hits);
@@ -171,6 +171,132 @@ void meta_analysis(void *idx, char *input, uint64_t input_n, char **output, uint
 	dsb_index *ix = idx;
 	thread_state(ix, thread_id, -1);
 	dsb_meta_analysis(ix, input, input_n, output, output_n, flag, max_snapshot_len, human_snapshot, human_snapshot_n);
+}
+
+/* ------------------------------------------------------------------ batch API */
+struct dsb_batch {
+	dsb_reads_t reads;
+	dsb_gpu_batch *g;
+};
+
+static void copy_timing(dsb_timing_t *t, const dsb_gpu_timing *gt)
+{
+	int st = t->stats_on;
+	memset(t, 0, sizeof(*t));
+	t->stats_on = st;
+	t->ms_total = gt->ms_total;
+	t->ms_h2d = gt->ms_h2d;
+	t->ms_d2h = gt->ms_d2h;
+	t->ms_encode = gt->ms_encode;
+	t->ms_seed = gt->ms_seed;
+	t->ms_classA = gt->ms_classA;
+	t->ms_classB = gt->ms_classB;
+	t->n_reads = gt->n_reads;
+	t->n_bases = gt->n_bases;
+	t->n_retry = gt->n_retry;
+	t->n_chunks = gt->n_chunks;
+	t->seed_positions = gt->seed_positions;
+	for (int k = 0; k < 32; k++) t->stats[k] = gt->stats[k];
+}
+
+dsb_batch *dsb_batch_create(void *idx, const char *text, uint64_t text_n, dsb_timing_t *timing)
+{
+	char err[1024];
+	dsb_batch *b = calloc(1, sizeof(*b));
+	dsb_parse_reads(text, text_n, &b->reads);
+	dsb_gpu_timing gt;
+	memset(&gt, 0, sizeof(gt));
+	if (dsb_gpu_batch_upload(idx, &b->reads, &b->g, &gt, err, sizeof(err))) {
+		fprintf(stderr, "[dsb_batch_create] %s\n", err);
+		dsb_reads_free(&b->reads);
+		free(b);
+		return NULL;
+	}
+	if (timing) copy_timing(timing, &gt);
+	return b;
+}
+
+int dsb_batch_run(void *idx, dsb_batch *b, int *max_read_l, dsb_timing_t *timing)
+{
+	char err[1024];
+	dsb_gpu_timing gt;
+	memset(&gt, 0, sizeof(gt));
+	int rc = dsb_gpu_batch_run(idx, b->g, max_read_l, timing ? timing->stats_on : 0, &gt, err, sizeof(err));
+	if (rc) fprintf(stderr, "[dsb_batch_run] %s\n", err);
+	if (timing) copy_timing(timing, &gt);
+	return rc;
+}
+
+int dsb_batch_format(void *idx, dsb_batch *b, int format, char **output, uint64_t *output_n)
+{
+	const dsb_read_out_t *ro = dsb_gpu_batch_ro(b->g);
+	const dsb_hit_out_t *hits = dsb_gpu_batch_hits(b->g);
+	dsb_str out = {0, 0, 0};
+	for (uint64_t i = 0; i < b->reads.n; i++)
+		dsb_format_read(&out, idx, &b->reads, i, ro + i, hits + ro[i].hit_off, format, 5);
+	*output_n = out.l;
+	*output = calloc(out.l + 1, 1);
+	if (out.l) memcpy(*output, out.s, out.l);
+	free(out.s);
+	return 0;
+}
+
+/* taxid of "tid|<taxid>|..." reference names (getOneSAM, src/cly_mt.c:778-786) */
+static uint32_t name_taxid(const char *name)
+{
+	const char *p = strchr(name, '|');
+	return p ? (uint32_t)strtoul(p + 1, NULL, 10) : 0;
+}
+
+int dsb_batch_taxa(void *idx, dsb_batch *b, int flag, uint32_t *tid_out, uint64_t *weight_out)
+{
+	dsb_index *ix = idx;
+	const dsb_read_out_t *ro = dsb_gpu_batch_ro(b->g);
+	const dsb_hit_out_t *hits = dsb_gpu_batch_hits(b->g);
+	uint32_t *rec_tid = malloc(sizeof(uint32_t) * (DSB_MAX_HITS + 1));
+	uint32_t *rec_score = malloc(sizeof(uint32_t) * (DSB_MAX_HITS + 1));
+	for (uint64_t i = 0; i < b->reads.n; i++) {
+		const dsb_rec_t *rec = b->reads.rec + i;
+		weight_out[i] = (flag & 1) ? (uint64_t)strlen(b->reads.arena + rec->seq_off) : 1;
+		uint32_t nh = ro[i].n_hit;
+		if (nh == 0) { tid_out[i] = 0; continue; }
+		const dsb_hit_out_t *h = hits + ro[i].hit_off;
+		/* SAM record order of output_one_result_sam: primary, supplementaries, secondaries */
+		uint32_t nr = 0;
+		rec_tid[nr] = name_taxid(ix->ref_name[h[0].ref_ID]); rec_score[nr++] = h[0].sum_score;
+		for (int loop = 0; loop <= 1; loop++)
+			for (uint32_t k = 1; k < nh; k++)
+				if ((loop == 0 && h[k].pri_index == 0) || (loop == 1 && h[k].pri_index > 0 && h[k].pri_index <= 5)) {
+					rec_tid[nr] = name_taxid(ix->ref_name[h[k].ref_ID]);
+					rec_score[nr++] = h[k].sum_score;
+				}
+		/* ana_get_tid: an equal-score later record of a descendant taxon wins */
+		uint32_t tid = 0, score = 0;
+		if (rec_tid[0] <= ix->max_tid) { tid = rec_tid[0]; score = rec_score[0]; }
+		for (uint32_t k = 1; k < nr && score != 0; k++) {
+			if (rec_score[k] != score || rec_tid[k] > ix->max_tid) continue;
+			for (uint32_t pt = rec_tid[k];; pt = ix->tax[pt].p_tid) {
+				if (pt == tid) { tid = rec_tid[k]; break; }
+				if (pt < 1 || pt == 4294967295u) break;
+			}
+		}
+		tid_out[i] = tid;
+	}
+	free(rec_tid);
+	free(rec_score);
+	return 0;
+}
+
+uint64_t dsb_batch_reads(dsb_batch *b) { return b->reads.n; }
+uint64_t dsb_batch_bases(dsb_batch *b) { return dsb_gpu_batch_bases(b->g); }
+uint64_t dsb_max_tid(void *idx) { return ((dsb_index *)idx)->max_tid; }
+
+void dsb_batch_free(void *idx, dsb_batch *b)
+{
+	if (!b) return;
+	dsb_gpu_batch_free(idx, b->g);
+	dsb_reads_free(&b->reads);
+	free(b);
 }
 
 /* ------------------------------------------------------------------ extensions */

@@ -106,6 +106,35 @@ typedef struct {
 enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, DSB_ST_REFPOS,
        DSB_ST_GETREF_B, DSB_ST_ANCHOR, DSB_ST_CHAIN, DSB_ST_EK1, DSB_ST_EK2, DSB_ST_N };
 
+/*
+ * Work accounting (stats kernels only; w->stats == 0 otherwise).  The byte figures are the
+ * algorithmic bytes of DESIGN.md §Roofline: 8 B checkpoint + the nibble bytes up to r in
+ * the 256-symbol occ block, 8 B per SA sample / unitig entry / ref_pos entry, 2 bits per
+ * reference base unpacked.
+ */
+DSB_HD void dsb_stat_occ(dsb_read_ws *w, uint64_t r)
+{
+	if (w->stats) {
+		w->stats[DSB_ST_OCC]++;
+		w->stats[DSB_ST_OCC_NIB] += 8 + 2 * (((r & 255) >> 2) + 1);
+	}
+}
+DSB_HD uint64_t dsb_lf_w(dsb_read_ws *w, uint64_t r, uint8_t *c)
+{
+	dsb_stat_occ(w, r);
+	return dsb_lf(w->ix, r, c);
+}
+DSB_HD uint64_t dsb_occ_w(dsb_read_ws *w, uint64_t r, uint8_t *c)
+{
+	dsb_stat_occ(w, r);
+	return dsb_occ(w->ix, r, c);
+}
+DSB_HD void dsb_get_ref_w(dsb_read_ws *w, uint8_t *ref_str, uint64_t uni_offset, uint32_t length, int isForward)
+{
+	if (w->stats) w->stats[DSB_ST_GETREF_B] += (length + 3) / 4;
+	dsb_get_ref(w->ix, ref_str, uni_offset, length, isForward);
+}
+
 DSB_HD int dsb_exist_bit(const uint64_t *ex, uint32_t k)
 {
 	return (int)((ex[k >> 6] >> (k & 63)) & 1);
@@ -242,8 +271,7 @@ DSB_HD void dsb_single_search(dsb_read_ws *w, uint64_t sp, const uint8_t *string
 		} else
 			sa_sp_l--;
 		uint8_t c;
-		new_sp = dsb_lf(ix, sp, &c);
-		if (w->stats) w->stats[DSB_ST_OCC]++;
+		new_sp = dsb_lf_w(w, sp, &c);
 		if (c != *string)
 			break;
 		match_len++;
@@ -275,9 +303,8 @@ DSB_HD int dsb_mem_search(dsb_read_ws *w, const uint8_t *string, uint64_t pre_v,
 		c = *string;
 		string--;
 		uint8_t c2 = c;
-		new_sp = ix->rank[c] + dsb_occ(ix, sp, &c);
-		new_ep = ix->rank[c2] + dsb_occ(ix, ep, &c2);
-		if (w->stats) w->stats[DSB_ST_OCC] += 2;
+		new_sp = ix->rank[c] + dsb_occ_w(w, sp, &c);
+		new_ep = ix->rank[c2] + dsb_occ_w(w, ep, &c2);
 		if (match_len >= l_min_mth - 1) {
 			if (new_sp + max_rst >= new_ep)
 				break;
@@ -330,6 +357,17 @@ DSB_HD uint32_t dsb_get_uni(const dsb_dindex_t *ix, uint64_t bwt_pos, int search
 	*uni_offset_ = uni_offset;
 	return u;
 }
+DSB_HD uint32_t dsb_get_uni_w(dsb_read_ws *w, uint64_t bwt_pos, int search_l, uint64_t *global_offset,
+			       uint32_t *uni_offset_)
+{
+	uint32_t u = dsb_get_uni(w->ix, bwt_pos, search_l, global_offset, uni_offset_);
+	if (w->stats) {
+		w->stats[DSB_ST_SA]++;
+		w->stats[DSB_ST_UNI] += 1 + (u - w->ix->sa[bwt_pos >> 3].unitig_ID);
+		w->stats[DSB_ST_REFPOS]++;
+	}
+	return u;
+}
 
 /* get_new_ed, src/cly.c:624-689 */
 DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t *len_, uint32_t *l_mem_ext,
@@ -351,7 +389,7 @@ DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t
 		len = DSB_MIN(12u, max_len);
 		q = q_b + q_off;
 	}
-	dsb_get_ref(w->ix, t, t_off, len, !is_FWD);
+	dsb_get_ref_w(w, t, t_off, len, !is_FWD);
 	if (len > 0 && t[0] == q[0]) {
 		int mtc;
 		do {
@@ -371,7 +409,7 @@ DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t
 					t_off += mtc;
 					q += mtc;
 				}
-				dsb_get_ref(w->ix, t, t_off, len, !is_FWD);
+				dsb_get_ref_w(w, t, t_off, len, !is_FWD);
 			}
 		} while (mtc > 0);
 	}
@@ -426,16 +464,14 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 			q_pre[k] = q_b[q_off - k];
 		int s_l = 0;
 		if (m_r->sa_sp != ~0ull) {
-			uni = (int32_t)dsb_get_uni(ix, m_r->sa_sp, m_r->sa_sp_l, &t_off, &u_off);
-			if (w->stats) w->stats[DSB_ST_SA]++;
+			uni = (int32_t)dsb_get_uni_w(w, m_r->sa_sp, m_r->sa_sp_l, &t_off, &u_off);
 		} else {
 			uint8_t c;
 			uint64_t new_sp;
 			while (1) {
 				if ((b_p & 7) == 0)
 					break;
-				new_sp = dsb_lf(ix, b_p, &c);
-				if (w->stats) w->stats[DSB_ST_OCC]++;
+				new_sp = dsb_lf_w(w, b_p, &c);
 				if (c == 4)
 					break;
 				t_pre[s_l++] = c;
@@ -444,8 +480,7 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 					break;
 			}
 			if ((b_p & 7) == 0) {
-				uni = (int32_t)dsb_get_uni(ix, b_p, s_l, &t_off, &u_off);
-				if (w->stats) w->stats[DSB_ST_SA]++;
+				uni = (int32_t)dsb_get_uni_w(w, b_p, s_l, &t_off, &u_off);
 			} else
 				l_pre = s_l;
 		}
@@ -453,7 +488,7 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 			if (ix->uni[uni].length < DSB_MIN_UNI_L)
 				break;
 			l_pre = DSB_MIN(l_pre, u_off);
-			dsb_get_ref(ix, t_pre, t_off - 1, l_pre, 0);
+			dsb_get_ref_w(w, t_pre, t_off - 1, l_pre, 0);
 		}
 		d_pre = dsb_lv_extd(t_pre, l_pre, q_pre, l_pre);
 		s = dsb_qmem(ix, l_m) + Q_LV[d_pre * DSB_LV_DIM + l_pre];
@@ -464,12 +499,10 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 		if (uni < 0) {
 			while (b_p & 7) {
 				uint8_t c;
-				b_p = dsb_lf(ix, b_p, &c);
-				if (w->stats) w->stats[DSB_ST_OCC]++;
+				b_p = dsb_lf_w(w, b_p, &c);
 				s_l++;
 			}
-			uni = (int32_t)dsb_get_uni(ix, b_p, s_l, &t_off, &u_off);
-			if (w->stats) w->stats[DSB_ST_SA]++;
+			uni = (int32_t)dsb_get_uni_w(w, b_p, s_l, &t_off, &u_off);
 			if (ix->uni[uni].length < DSB_MIN_UNI_L) {
 				s = 0;
 				break;
@@ -480,7 +513,7 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 		if (l_max_suf != 0) {
 			l_suf = DSB_MIN(l_max_suf, (uint32_t)DSB_LV_L);
 			q_suf = q_b + q_off_r;
-			dsb_get_ref(ix, t_suf, t_off + l_m, l_suf, 1);
+			dsb_get_ref_w(w, t_suf, t_off + l_m, l_suf, 1);
 			if (t_suf[0] == q_suf[0]) {
 				int mtc;
 				do {
@@ -493,7 +526,7 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 						l_max_suf -= mtc;
 						l_suf = DSB_MIN(l_max_suf, (uint32_t)DSB_LV_L);
 						q_suf += mtc;
-						dsb_get_ref(ix, t_suf, t_off + l_m, l_suf, 1);
+						dsb_get_ref_w(w, t_suf, t_off + l_m, l_suf, 1);
 					}
 				} while (mtc > 0);
 			}
@@ -694,6 +727,7 @@ DSB_HD dsb_chain_t *dsb_push_chain(dsb_read_ws *w)
 		w->overflow |= 4;
 		return 0;
 	}
+	if (w->stats) w->stats[DSB_ST_CHAIN]++;
 	return w->hit + w->n_hit++;
 }
 
@@ -1084,7 +1118,7 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 					w->overflow |= 32;
 					return 0;
 				}
-				dsb_get_ref(ix, ref, (uint64_t)(int64_t)(pre_refoffset + pre_mch) + t_offset, (uint32_t)total_ref_len, 1);
+				dsb_get_ref_w(w, ref, (uint64_t)(int64_t)(pre_refoffset + pre_mch) + t_offset, (uint32_t)total_ref_len, 1);
 				for (int k = total_ref_len; k < 2000 + 64; k++) ref[k] = DSB_STACK_PATTERN;
 				dsb_sdp_match(w, pre_a->index_in_read + pre_mch - 8, c_a->index_in_read - 1, q_str, ref,
 					      (uint32_t)total_ref_len, key_len, hslot, (uint32_t)(pre_refoffset + pre_mch), 1);
@@ -1199,7 +1233,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 			} else
 				max_search_ref = (uint32_t)(t_length - c_t_offset);
 			max_search_ref = DSB_MIN(600u, max_search_ref);
-			dsb_get_ref(ix, ref, c_t_offset + t_offset_global, max_search_ref + DSB_OVER_SEARCH, 1);
+			dsb_get_ref_w(w, ref, c_t_offset + t_offset_global, max_search_ref + DSB_OVER_SEARCH, 1);
 			int search_q_ed = (int)w->sms[max_sms_id].q_pos + 1000;
 			search_q_ed = DSB_MIN(search_q_ed, l_read);                /* int vs uint32: unsigned */
 			int search_q_st = DSB_MAX(search_q_ed - 2000, c_h->q_st - 8); /* idem (H11) */
@@ -1303,9 +1337,9 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 				max_search_ref = c_t_offset;
 			max_search_ref = DSB_MIN(600u, max_search_ref);
 			if (t_offset_global == 0 && c_t_offset < DSB_OVER_SEARCH + max_search_ref)
-				dsb_get_ref(ix, ref, c_t_offset + t_offset_global - max_search_ref, max_search_ref, 1);
+				dsb_get_ref_w(w, ref, c_t_offset + t_offset_global - max_search_ref, max_search_ref, 1);
 			else
-				dsb_get_ref(ix, ref, c_t_offset + t_offset_global - max_search_ref - DSB_OVER_SEARCH,
+				dsb_get_ref_w(w, ref, c_t_offset + t_offset_global - max_search_ref - DSB_OVER_SEARCH,
 					    max_search_ref + DSB_OVER_SEARCH, 1);
 			int search_q_st = (int)w->sms[max_sms_id].q_pos - 1000;
 			search_q_st = DSB_MAX(search_q_st, 0);

@@ -14,13 +14,16 @@ extern "C" {
 
 #define DSB_MAX_HITS 400 /* delete_small_score_rst keeps at most 400 chains (src/cly.c:2892) */
 
+#define DSB_N_STATS 32
+#define DSB_STATS_B 16
+
 typedef struct {
 	double ms_total;      /* wall time of dsb_gpu_classify, host-measured */
 	double ms_h2d, ms_d2h;
 	double ms_encode, ms_seed, ms_classA, ms_classB; /* HIP-event kernel times, summed over chunks */
 	uint64_t n_reads, n_bases, n_retry, n_chunks;
 	uint64_t seed_positions; /* k-mer positions probed by the seed kernel (both strands) */
-	uint64_t stats[16];   /* algorithmic-work counters (DSB_ST_*), when enabled */
+	uint64_t stats[DSB_N_STATS]; /* work counters (DSB_ST_*): [0,16) k_classA, [16,32) k_classB */
 } dsb_gpu_timing;
 
 /* Upload the index to `device` (-1: DSB_DEVICE env var, else the current HIP device).
@@ -34,6 +37,18 @@ void dsb_gpu_free(dsb_index *ix);
 int dsb_gpu_classify(dsb_index *ix, const dsb_reads_t *reads, int *max_read_l, dsb_read_out_t *ro,
 		     dsb_hit_out_t **hits, uint64_t *n_hits, int stats_on, dsb_gpu_timing *timing, char *err,
 		     size_t errn);
+
+/* Batches: reads resident in HBM, classified by one or more runs. */
+typedef struct dsb_gpu_batch dsb_gpu_batch;
+int dsb_gpu_batch_upload(dsb_index *ix, const dsb_reads_t *reads, dsb_gpu_batch **b, dsb_gpu_timing *timing,
+			 char *err, size_t errn);
+int dsb_gpu_batch_run(dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on, dsb_gpu_timing *timing,
+		      char *err, size_t errn);
+const dsb_read_out_t *dsb_gpu_batch_ro(const dsb_gpu_batch *b);
+const dsb_hit_out_t *dsb_gpu_batch_hits(const dsb_gpu_batch *b);
+uint64_t dsb_gpu_batch_n(const dsb_gpu_batch *b);
+uint64_t dsb_gpu_batch_bases(const dsb_gpu_batch *b);
+void dsb_gpu_batch_free(dsb_index *ix, dsb_gpu_batch *b);
 
 /* Number of visible devices (0 if HIP has none). */
 int dsb_gpu_device_count(void);

@@ -144,12 +144,13 @@ __global__ __launch_bounds__(64) void k_classA(const dsb_dindex_t *__restrict__ 
 			atomicAdd(gstats + k, (unsigned long long)st[k]);
 }
 
+template <bool STATS>
 __global__ __launch_bounds__(64) void k_classB(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 						const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 						uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 						const int32_t *__restrict__ mrl, dsb_read_out_t *__restrict__ ro,
 						dsb_hit_out_t *__restrict__ hits_out, uint32_t *__restrict__ hit_cursor,
-						uint32_t *__restrict__ hit_off)
+						uint32_t *__restrict__ hit_off, unsigned long long *__restrict__ gstats)
 {
 	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= n)
@@ -164,6 +165,11 @@ __global__ __launch_bounds__(64) void k_classB(const dsb_dindex_t *__restrict__ 
 	w.fast_classify = o.fast;
 	w.overflow = o.status;
 	w.reached_update = o.reached_update;
+	uint64_t st[DSB_ST_N];
+	if (STATS) {
+		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
+		w.stats = st;
+	}
 	/* hits are staged in the read's own hit_tmp region, then compacted */
 	dsb_hit_out_t *stage = (dsb_hit_out_t *)w.hit_tmp;
 	dsb_classify_B(&w, mrl[r], &o, stage, DSB_MAX_HITS);
@@ -173,6 +179,9 @@ __global__ __launch_bounds__(64) void k_classB(const dsb_dindex_t *__restrict__ 
 	hit_off[r] = off;
 	o.hit_off = off;
 	ro[r] = o;
+	if (STATS)
+		for (int k = 0; k < DSB_ST_N; k++)
+			atomicAdd(gstats + DSB_STATS_B + k, (unsigned long long)st[k]);
 }
 
 /* The merge-sort orders the classifier depends on, one array per lane:
@@ -244,6 +253,7 @@ struct dbuf {
 		cap = 0;
 	}
 	template <typename T> T *as() const { return (T *)p; }
+	~dbuf() { release(); }
 };
 
 struct dsb_gpu_dev {
@@ -254,7 +264,7 @@ struct dsb_gpu_dev {
 	dsb_dindex_t h;          /* host copy holding device pointers */
 	dsb_dindex_t *d;         /* device copy */
 	std::vector<void *> allocs;
-	dbuf seq, seq_off, len, ws_off, scale, ws, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2;
+	dbuf ws_off, scale, ws, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2;
 };
 
 template <typename T>
@@ -349,8 +359,8 @@ extern "C" void dsb_gpu_free(dsb_index *ix)
 	hipSetDevice(g->device);
 	for (void *p : g->allocs)
 		hipFree(p);
-	dbuf *bs[] = {&g->seq, &g->seq_off, &g->len, &g->ws_off, &g->scale, &g->ws, &g->order, &g->word_off,
-		      &g->ro, &g->mrl, &g->hits, &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2};
+	dbuf *bs[] = {&g->ws_off, &g->scale, &g->ws, &g->order, &g->word_off, &g->ro, &g->mrl, &g->hits,
+		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2};
 	for (dbuf *b : bs)
 		b->release();
 	hipEventDestroy(g->ev_a);
@@ -410,49 +420,75 @@ static uint64_t seed_words(const std::vector<uint32_t> &len, uint64_t cb, const 
 	return tw;
 }
 
-static int classify_locked(dsb_gpu_dev *g, dsb_index *ix, const dsb_reads_t *reads, int *max_read_l,
-			   dsb_read_out_t *ro, std::vector<dsb_hit_out_t> &hv, int stats_on, dsb_gpu_timing &T, char *err,
-			   size_t errn)
+/* a batch of reads resident in HBM (sequences only) + its results */
+struct dsb_gpu_batch {
+	uint64_t n = 0, tot = 0;
+	std::vector<uint32_t> len;
+	std::vector<uint64_t> seq_off;
+	dbuf seq, d_seq_off, d_len;
+	std::vector<dsb_read_out_t> ro;
+	std::vector<dsb_hit_out_t> hits;
+};
+
+static int batch_upload(dsb_gpu_dev *g, const dsb_reads_t *reads, dsb_gpu_batch *b, dsb_gpu_timing &T, char *err,
+			size_t errn)
 {
 	HIP_OK(hipSetDevice(g->device));
 	hipStream_t s = g->stream;
 	uint64_t n = reads->n;
-	/* ---- reads: bases only, concatenated */
-	std::vector<uint64_t> seq_off(n);
-	std::vector<uint32_t> len(n);
+	b->n = n;
+	b->len.resize(n);
+	b->seq_off.resize(n);
 	uint64_t tot = 0;
 	for (uint64_t i = 0; i < n; i++) {
-		seq_off[i] = tot;
-		len[i] = reads->rec[i].seq_l;
-		tot += len[i];
+		b->seq_off[i] = tot;
+		b->len[i] = reads->rec[i].seq_l;
+		tot += b->len[i];
 	}
-	T.n_bases = tot;
-	if (n == 0)
-		return 0;
-	if (g->seq.ensure(tot + 16, err, errn) || g->seq_off.ensure(8 * n + 8, err, errn) ||
-	    g->len.ensure(4 * n + 4, err, errn) || g->scale.ensure(4 * n + 4, err, errn) ||
-	    g->ro.ensure(sizeof(dsb_read_out_t) * n + 64, err, errn) || g->mrl.ensure(4 * n + 4, err, errn) ||
-	    g->hit_off.ensure(4 * n + 4, err, errn) || g->cnt.ensure(64, err, errn) || g->stats.ensure(8 * 16, err, errn) ||
-	    g->ws_off.ensure(8 * n + 8, err, errn))
+	b->tot = tot;
+	if (b->seq.ensure(tot + 16, err, errn) || b->d_seq_off.ensure(8 * n + 8, err, errn) ||
+	    b->d_len.ensure(4 * n + 4, err, errn))
 		return -1;
 	double th = now_ms();
-	{
-		std::vector<uint8_t> stage(tot + 16); /* pack sequences (the arena also holds names/quals) */
-		for (uint64_t i = 0; i < n; i++)
-			memcpy(stage.data() + seq_off[i], reads->arena + reads->rec[i].seq_off, len[i]);
-		HIP_OK(hipMemcpyAsync(g->seq.p, stage.data(), tot, hipMemcpyHostToDevice, s));
-		HIP_OK(hipMemcpyAsync(g->seq_off.p, seq_off.data(), 8 * n, hipMemcpyHostToDevice, s));
-		HIP_OK(hipMemcpyAsync(g->len.p, len.data(), 4 * n, hipMemcpyHostToDevice, s));
-		HIP_OK(hipStreamSynchronize(s));
-	}
+	std::vector<uint8_t> stage(tot + 16); /* pack the bases (the arena also holds names/quals) */
+	for (uint64_t i = 0; i < n; i++)
+		memcpy(stage.data() + b->seq_off[i], reads->arena + reads->rec[i].seq_off, b->len[i]);
+	HIP_OK(hipMemcpyAsync(b->seq.p, stage.data(), tot, hipMemcpyHostToDevice, s));
+	HIP_OK(hipMemcpyAsync(b->d_seq_off.p, b->seq_off.data(), 8 * n, hipMemcpyHostToDevice, s));
+	HIP_OK(hipMemcpyAsync(b->d_len.p, b->len.data(), 4 * n, hipMemcpyHostToDevice, s));
+	HIP_OK(hipStreamSynchronize(s));
 	T.ms_h2d += now_ms() - th;
-	HIP_OK(hipMemsetAsync(g->stats.p, 0, 8 * 16, s));
+	T.n_reads = n;
+	T.n_bases = tot;
+	return 0;
+}
+
+static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on,
+		     dsb_gpu_timing &T, char *err, size_t errn)
+{
+	HIP_OK(hipSetDevice(g->device));
+	hipStream_t s = g->stream;
+	uint64_t n = b->n;
+	const std::vector<uint32_t> &len = b->len;
+	T.n_reads = n;
+	T.n_bases = b->tot;
+	b->ro.assign(n, dsb_read_out_t());
+	b->hits.clear();
+	if (n == 0)
+		return 0;
+	if (g->scale.ensure(4 * n + 4, err, errn) || g->ro.ensure(sizeof(dsb_read_out_t) * n + 64, err, errn) ||
+	    g->mrl.ensure(4 * n + 4, err, errn) || g->hit_off.ensure(4 * n + 4, err, errn) ||
+	    g->cnt.ensure(64, err, errn) || g->stats.ensure(8 * DSB_N_STATS, err, errn) || g->ws_off.ensure(8 * n + 8, err, errn))
+		return -1;
+	HIP_OK(hipMemsetAsync(g->stats.p, 0, 8 * DSB_N_STATS, s));
 	std::vector<uint32_t> scale(n, 1);
 	std::vector<uint64_t> ws_off(n);
 	std::vector<dsb_read_out_t> h_ro(n);
 	std::vector<int32_t> mrl(n);
 	std::vector<uint32_t> hit_off(n);
 	std::vector<uint64_t> word_off;
+	dsb_read_out_t *ro = b->ro.data();
+	std::vector<dsb_hit_out_t> &hv = b->hits;
 	size_t budget = ws_budget();
 	int carry = *max_read_l;
 	int l_ek = ix->l_ek;
@@ -474,8 +510,8 @@ static int classify_locked(dsb_gpu_dev *g, dsb_index *ix, const dsb_reads_t *rea
 			return -1;
 		HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
 		HIP_OK(hipMemcpyAsync(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
-		const uint32_t *cl = g->len.as<uint32_t>() + cb;
-		const uint64_t *cso = g->seq_off.as<uint64_t>() + cb;
+		const uint32_t *cl = b->d_len.as<uint32_t>() + cb;
+		const uint64_t *cso = b->d_seq_off.as<uint64_t>() + cb;
 		/* length-sorted order (longest first) for the one-lane-per-read kernels */
 		std::vector<uint32_t> order(cn);
 		for (uint32_t i = 0; i < cn; i++) order[i] = i;
@@ -485,7 +521,7 @@ static int classify_locked(dsb_gpu_dev *g, dsb_index *ix, const dsb_reads_t *rea
 		HIP_OK(hipMemcpyAsync(g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
 		uint8_t *wsb = g->ws.as<uint8_t>();
 		hipEventRecord(g->ev_a, s);
-		k_encode<<<cn, 256, 0, s>>>(g->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, nullptr, cn);
+		k_encode<<<cn, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, nullptr, cn);
 		T.ms_encode += ev_ms(g);
 		HIP_OK(hipGetLastError());
 		if (tw) {
@@ -547,7 +583,7 @@ static int classify_locked(dsb_gpu_dev *g, dsb_index *ix, const dsb_reads_t *rea
 			HIP_OK(hipMemcpyAsync(g->sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, s));
 			HIP_OK(hipMemcpyAsync(g->wo2.p, wo2.data(), 8 * wo2.size(), hipMemcpyHostToDevice, s));
 			uint32_t m = (uint32_t)sel.size();
-			k_encode<<<m, 256, 0, s>>>(g->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, g->sel.as<uint32_t>(), m);
+			k_encode<<<m, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, g->sel.as<uint32_t>(), m);
 			if (tw2)
 				k_seed<<<(uint32_t)((tw2 * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
 											      g->wo2.as<uint64_t>(), g->sel.as<uint32_t>(), m, tw2);
@@ -590,9 +626,14 @@ static int classify_locked(dsb_gpu_dev *g, dsb_index *ix, const dsb_reads_t *rea
 			return -1;
 		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
 		hipEventRecord(g->ev_a, s);
-		k_classB<<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
+		if (stats_on)
+			k_classB<true><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
 							 g->order.as<uint32_t>(), cn, g->mrl.as<int32_t>(), g->ro.as<dsb_read_out_t>(),
-							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>());
+							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(), g->stats.as<unsigned long long>());
+		else
+			k_classB<false><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
+							 g->order.as<uint32_t>(), cn, g->mrl.as<int32_t>(), g->ro.as<dsb_read_out_t>(),
+							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(), g->stats.as<unsigned long long>());
 		T.ms_classB += ev_ms(g);
 		HIP_OK(hipGetLastError());
 		double td = now_ms();
@@ -611,16 +652,42 @@ static int classify_locked(dsb_gpu_dev *g, dsb_index *ix, const dsb_reads_t *rea
 	}
 	*max_read_l = carry;
 	if (stats_on) {
-		unsigned long long st[16];
+		unsigned long long st[DSB_N_STATS];
 		HIP_OK(hipMemcpy(st, g->stats.p, sizeof(st), hipMemcpyDeviceToHost));
-		for (int k = 0; k < 16; k++) T.stats[k] = st[k];
+		for (int k = 0; k < DSB_N_STATS; k++) T.stats[k] = st[k];
 	}
 	return 0;
 }
 
-extern "C" int dsb_gpu_classify(dsb_index *ix, const dsb_reads_t *reads, int *max_read_l, dsb_read_out_t *ro,
-				dsb_hit_out_t **hits, uint64_t *n_hits, int stats_on, dsb_gpu_timing *tm, char *err,
-				size_t errn)
+extern "C" int dsb_gpu_batch_upload(dsb_index *ix, const dsb_reads_t *reads, dsb_gpu_batch **out, dsb_gpu_timing *tm,
+				    char *err, size_t errn)
+{
+	dsb_gpu_dev *g = (dsb_gpu_dev *)ix->gpu;
+	if (!g) {
+		snprintf(err, errn, "index not resident on a GPU (dsb_gpu_init not called)");
+		return -1;
+	}
+	dsb_gpu_timing T;
+	memset(&T, 0, sizeof(T));
+	dsb_gpu_batch *b = new dsb_gpu_batch();
+	pthread_mutex_lock(&g->mu);
+	int rc = batch_upload(g, reads, b, T, err, errn);
+	pthread_mutex_unlock(&g->mu);
+	if (tm) {
+		tm->ms_h2d += T.ms_h2d;
+		tm->n_reads = T.n_reads;
+		tm->n_bases = T.n_bases;
+	}
+	if (rc) {
+		delete b;
+		return rc;
+	}
+	*out = b;
+	return 0;
+}
+
+extern "C" int dsb_gpu_batch_run(dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on, dsb_gpu_timing *tm,
+				 char *err, size_t errn)
 {
 	dsb_gpu_dev *g = (dsb_gpu_dev *)ix->gpu;
 	if (!g) {
@@ -630,15 +697,54 @@ extern "C" int dsb_gpu_classify(dsb_index *ix, const dsb_reads_t *reads, int *ma
 	double t0 = now_ms();
 	dsb_gpu_timing T;
 	memset(&T, 0, sizeof(T));
-	T.n_reads = reads->n;
 	pthread_mutex_lock(&g->mu);
-	std::vector<dsb_hit_out_t> hv;
-	int rc = classify_locked(g, ix, reads, max_read_l, ro, hv, stats_on, T, err, errn);
+	int rc = batch_run(g, ix, b, max_read_l, stats_on, T, err, errn);
 	pthread_mutex_unlock(&g->mu);
-	*n_hits = hv.size();
-	*hits = (dsb_hit_out_t *)malloc(sizeof(dsb_hit_out_t) * (hv.size() + 1));
-	if (*hits && !hv.empty())
-		memcpy(*hits, hv.data(), sizeof(dsb_hit_out_t) * hv.size());
+	T.ms_total = now_ms() - t0;
+	if (tm) {
+		double h2d = tm->ms_h2d;
+		*tm = T;
+		tm->ms_h2d += h2d;
+	}
+	return rc;
+}
+
+extern "C" const dsb_read_out_t *dsb_gpu_batch_ro(const dsb_gpu_batch *b) { return b->ro.data(); }
+extern "C" const dsb_hit_out_t *dsb_gpu_batch_hits(const dsb_gpu_batch *b) { return b->hits.data(); }
+extern "C" uint64_t dsb_gpu_batch_n(const dsb_gpu_batch *b) { return b->n; }
+extern "C" uint64_t dsb_gpu_batch_bases(const dsb_gpu_batch *b) { return b->tot; }
+
+extern "C" void dsb_gpu_batch_free(dsb_index *ix, dsb_gpu_batch *b)
+{
+	dsb_gpu_dev *g = ix ? (dsb_gpu_dev *)ix->gpu : nullptr;
+	if (g) {
+		pthread_mutex_lock(&g->mu);
+		hipSetDevice(g->device);
+	}
+	delete b;
+	if (g)
+		pthread_mutex_unlock(&g->mu);
+}
+
+extern "C" int dsb_gpu_classify(dsb_index *ix, const dsb_reads_t *reads, int *max_read_l, dsb_read_out_t *ro,
+				dsb_hit_out_t **hits, uint64_t *n_hits, int stats_on, dsb_gpu_timing *tm, char *err,
+				size_t errn)
+{
+	dsb_gpu_timing T;
+	memset(&T, 0, sizeof(T));
+	dsb_gpu_batch *b = nullptr;
+	double t0 = now_ms();
+	if (dsb_gpu_batch_upload(ix, reads, &b, &T, err, errn))
+		return -1;
+	int rc = dsb_gpu_batch_run(ix, b, max_read_l, stats_on, &T, err, errn);
+	if (rc == 0) {
+		memcpy(ro, b->ro.data(), sizeof(dsb_read_out_t) * b->n);
+		*n_hits = b->hits.size();
+		*hits = (dsb_hit_out_t *)malloc(sizeof(dsb_hit_out_t) * (b->hits.size() + 1));
+		if (!b->hits.empty())
+			memcpy(*hits, b->hits.data(), sizeof(dsb_hit_out_t) * b->hits.size());
+	}
+	dsb_gpu_batch_free(ix, b);
 	T.ms_total = now_ms() - t0;
 	if (tm)
 		*tm = T;

@@ -21,11 +21,12 @@ class Timing(C.Structure):
                 ("ms_d2h", C.c_double), ("ms_encode", C.c_double), ("ms_seed", C.c_double),
                 ("ms_classA", C.c_double), ("ms_classB", C.c_double), ("n_reads", C.c_uint64),
                 ("n_bases", C.c_uint64), ("n_retry", C.c_uint64), ("n_chunks", C.c_uint64),
-                ("seed_positions", C.c_uint64), ("stats", C.c_uint64 * 16)]
+                ("seed_positions", C.c_uint64), ("stats", C.c_uint64 * 32)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("stats", "pad")}
         d["stats"] = {n: int(self.stats[i]) for i, n in enumerate(ST_NAMES)}
+        d["stats_B"] = {n: int(self.stats[16 + i]) for i, n in enumerate(ST_NAMES)}
         return d
 
 
@@ -52,6 +53,21 @@ def lib(path: str | None = None):
     L.dsb_classify_text.argtypes = [vp, C.c_char_p, u64, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_void_p), u64p,
                                     C.POINTER(Timing)]
     L.dsb_classify_text.restype = C.c_int
+    L.dsb_batch_create.argtypes = [vp, C.c_char_p, u64, C.POINTER(Timing)]
+    L.dsb_batch_create.restype = vp
+    L.dsb_batch_run.argtypes = [vp, vp, C.POINTER(C.c_int), C.POINTER(Timing)]
+    L.dsb_batch_run.restype = C.c_int
+    L.dsb_batch_format.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_void_p), u64p]
+    L.dsb_batch_format.restype = C.c_int
+    L.dsb_batch_taxa.argtypes = [vp, vp, C.c_int, C.c_void_p, C.c_void_p]
+    L.dsb_batch_taxa.restype = C.c_int
+    L.dsb_batch_reads.argtypes = [vp]
+    L.dsb_batch_reads.restype = u64
+    L.dsb_batch_bases.argtypes = [vp]
+    L.dsb_batch_bases.restype = u64
+    L.dsb_batch_free.argtypes = [vp, vp]
+    L.dsb_max_tid.argtypes = [vp]
+    L.dsb_max_tid.restype = u64
     L.dsb_version.restype = C.c_char_p
     L.dsb_device_count.restype = C.c_int
     L.dsb_free.argtypes = [vp]
@@ -99,6 +115,13 @@ class Index:
             raise RuntimeError("dsb_classify_text failed")
         return _take(self.L, out, n.value), t.as_dict(), mrl.value
 
+    def batch(self, data: bytes) -> "Batch":
+        """Parse + upload reads once; they stay resident in HBM for repeated runs."""
+        return Batch(self, data)
+
+    def max_tid(self) -> int:
+        return int(self.L.dsb_max_tid(self.h))
+
     def meta_analysis(self, sam: bytes, flag: int = 0, max_snapshot_len: int = 65536, thread_id: int = 0):
         out, n = C.c_void_p(), C.c_uint64(0)
         snap, sn = C.c_void_p(), C.c_uint64(0)
@@ -109,4 +132,47 @@ class Index:
     def close(self):
         if self.h:
             self.L.dsb_unload_index(self.h)
+            self.h = None
+
+
+class Batch:
+    """Reads resident in HBM (include/desamba_mi355x.h dsb_batch_*)."""
+
+    def __init__(self, index: Index, data: bytes):
+        self.ix, self.L = index, index.L
+        t = Timing()
+        self.h = self.L.dsb_batch_create(index.h, data, len(data), C.byref(t))
+        if not self.h:
+            raise RuntimeError("dsb_batch_create failed")
+        self.upload = t.as_dict()
+        self.n_reads = int(self.L.dsb_batch_reads(self.h))
+        self.n_bases = int(self.L.dsb_batch_bases(self.h))
+        self.max_read_l = 0
+
+    def run(self, max_read_l: int | None = None, stats: bool = False) -> dict:
+        """Classify every read of the batch; returns the timing dict."""
+        mrl = C.c_int(self.max_read_l if max_read_l is None else max_read_l)
+        t = Timing()
+        t.stats_on = 1 if stats else 0
+        if self.L.dsb_batch_run(self.ix.h, self.h, C.byref(mrl), C.byref(t)) != 0:
+            raise RuntimeError("dsb_batch_run failed")
+        self.max_read_l = mrl.value
+        return t.as_dict()
+
+    def format(self, fmt: int = FMT_SAM) -> bytes:
+        out, n = C.c_void_p(), C.c_uint64(0)
+        self.L.dsb_batch_format(self.ix.h, self.h, fmt, C.byref(out), C.byref(n))
+        return _take(self.L, out, n.value)
+
+    def taxa(self, flag: int = 0):
+        """-> (tid uint32[n], weight uint64[n]) as meta_analysis assigns them."""
+        import numpy as np
+        tid = np.zeros(self.n_reads, dtype=np.uint32)
+        w = np.zeros(self.n_reads, dtype=np.uint64)
+        self.L.dsb_batch_taxa(self.ix.h, self.h, flag, tid.ctypes.data, w.ctypes.data)
+        return tid, w
+
+    def close(self):
+        if self.h:
+            self.L.dsb_batch_free(self.ix.h, self.h)
             self.h = None

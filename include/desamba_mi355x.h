@@ -18,7 +18,7 @@ typedef struct {
 	double ms_encode, ms_seed, ms_classA, ms_classB; /* per-kernel HIP-event times */
 	uint64_t n_reads, n_bases, n_retry, n_chunks;
 	uint64_t seed_positions; /* k-mer positions probed by k_seed (both strands) */
-	uint64_t stats[16];    /* DSB_ST_* counters (occ, MEM searches, SA lookups, ...) */
+	uint64_t stats[32];    /* work counters: [0,16) k_classA, [16,32) k_classB */
 } dsb_timing_t;
 
 /* Classify FASTQ/FASTA text.  format: 1 SAM, 2 SAM_FULL, 3 DES, 4 DES_FULL.
@@ -26,6 +26,21 @@ typedef struct {
  * *output is malloc'd (free with free()/dsb_free).  timing may be NULL.  Returns 0. */
 int dsb_classify_text(void *idx, const char *text, uint64_t text_n, int format, int *max_read_l, char **output,
 		      uint64_t *output_n, dsb_timing_t *timing);
+
+/* Batch API: parse + upload once (reads resident in HBM), classify any number of times,
+ * format or reduce the results.  Used by bench.py to time the path with inputs in HBM. */
+typedef struct dsb_batch dsb_batch;
+dsb_batch *dsb_batch_create(void *idx, const char *text, uint64_t text_n, dsb_timing_t *timing);
+int dsb_batch_run(void *idx, dsb_batch *b, int *max_read_l, dsb_timing_t *timing);
+int dsb_batch_format(void *idx, dsb_batch *b, int format, char **output, uint64_t *output_n);
+/* Per-read taxon as meta_analysis assigns it (ana_get_tid, reference src/cly_mt.c:902-961):
+ * tid_out[i] (0 = unclassified); weight_out[i] = 1 or the read length (flag & 1). */
+int dsb_batch_taxa(void *idx, dsb_batch *b, int flag, uint32_t *tid_out, uint64_t *weight_out);
+uint64_t dsb_batch_reads(dsb_batch *b);
+uint64_t dsb_batch_bases(dsb_batch *b);
+void dsb_batch_free(void *idx, dsb_batch *b);
+/* largest taxid of the loaded taxonomy (+1e6, reference src/cly_mt.c:613) */
+uint64_t dsb_max_tid(void *idx);
 
 const char *dsb_version(void);
 int dsb_device_count(void);

@@ -7,7 +7,7 @@
  * libdesamba.so (whose classify path exists only as HIP kernels) and never used by
  * bench.py's timed leg.
  *
- * usage: emu_classify [--dump-seeds] [--stats] <index_dir> <reads.fq>  > out.sam
+ * usage: emu_classify [--stats] [--des|--sam] <index_dir> <reads.fq>  > out.sam
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -25,10 +25,11 @@ int main(int argc, char **argv)
 	for (; ai < argc && argv[ai][0] == '-'; ai++) {
 		if (!strcmp(argv[ai], "--stats")) stats = 1;
 		else if (!strcmp(argv[ai], "--des")) fmt = DSB_OUT_DES;
+		else if (!strcmp(argv[ai], "--sam")) fmt = DSB_OUT_SAM;
 		else { fprintf(stderr, "unknown option %s\n", argv[ai]); return 2; }
 	}
 	if (ai + 2 > argc) {
-		fprintf(stderr, "usage: %s [--stats] [--des] <index_dir> <reads>\n", argv[0]);
+		fprintf(stderr, "usage: %s [--stats] [--des|--sam] <index_dir> <reads>\n", argv[0]);
 		return 2;
 	}
 	static dsb_index ix;
