@@ -256,6 +256,7 @@ def main():
             "classified_reads": classified,
             "phase_ms": {k: round(sum(t[k] for t in tms) / a.steps, 2)
                          for k in ("ms_encode", "ms_seed", "ms_classA", "ms_classB", "ms_d2h", "ms_total")},
+            "phase_ms_classA": {k: round(sum(t["ms_phase"][k] for t in tms) / a.steps, 2) for k in tms[0]["ms_phase"]},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

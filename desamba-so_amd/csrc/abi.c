@@ -118,6 +118,7 @@ int dsb_classify_text(void *idx, const char *text, uint64_t text_n, int format, 
 		timing->ms_seed = gt.ms_seed;
 		timing->ms_classA = gt.ms_classA;
 		timing->ms_classB = gt.ms_classB;
+		for (int k = 0; k < 12; k++) timing->ms_phase[k] = gt.ms_phase[k];
 		timing->n_reads = gt.n_reads;
 		timing->n_bases = gt.n_bases;
 		timing->n_retry = gt.n_retry;
@@ -191,6 +192,7 @@ static void copy_timing(dsb_timing_t *t, const dsb_gpu_timing *gt)
 	t->ms_seed = gt->ms_seed;
 	t->ms_classA = gt->ms_classA;
 	t->ms_classB = gt->ms_classB;
+	for (int k = 0; k < 12; k++) t->ms_phase[k] = gt->ms_phase[k];
 	t->n_reads = gt->n_reads;
 	t->n_bases = gt->n_bases;
 	t->n_retry = gt->n_retry;

@@ -9,6 +9,7 @@
 #ifndef DSB_CLASSIFY_H
 #define DSB_CLASSIFY_H
 #include "dsb_core.h"
+#include "dsb_wave.h"
 
 /* ------------------------------------------------------------------ per-read types */
 typedef struct { uint32_t offset, len; uint8_t top, p0, p1, p2; } dsb_seed_t; /* CLY_seed, cly.h:27-32 */
@@ -101,6 +102,7 @@ typedef struct {
 	uint32_t reached_update;
 	/* optional counters for algorithmic-byte accounting (bench) */
 	uint64_t *stats;
+	uint32_t dbg;           /* diagnostics: force sequential variants of the wave loops */
 } dsb_read_ws;
 
 enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, DSB_ST_REFPOS,
@@ -930,6 +932,38 @@ DSB_HDN void dsb_resolve_tree(dsb_read_ws *w)
 }
 
 /* ------------------------------------------------------------------ scoring (M2) */
+/* get_ref forward into an SDP window; WAVE: lanes unpack strided bases, then barrier */
+template <bool WAVE>
+DSB_HD void dsb_get_ref_win(dsb_read_ws *w, uint8_t *ref_str, uint64_t uni_offset, uint32_t length)
+{
+	if (!WAVE || (w->dbg & 8)) {
+		dsb_get_ref_w(w, ref_str, uni_offset, length, 1);
+	} else {
+		uint32_t lane = dsb_lane();
+		if (w->stats && lane == 0) w->stats[DSB_ST_GETREF_B] += (length + 3) / 4;
+		uint64_t b0 = uni_offset >> 2;
+		uint32_t odd = (uint32_t)(uni_offset & 3);
+		for (uint32_t k = lane; k < length; k += DSB_WV) {
+			uint32_t pos = odd + k;
+			uint8_t b = dsb_ref_byte(w->ix, b0 + (pos >> 2));
+			ref_str[k] = (b >> (6 - 2 * (pos & 3))) & 0x3;
+		}
+		dsb_wsync();
+	}
+}
+
+/* fill ref[lo, hi) with the stack pattern */
+template <bool WAVE>
+DSB_HD void dsb_fill_pattern(uint8_t *ref, int lo, int hi)
+{
+	if constexpr (!WAVE) {
+		for (int k = lo; k < hi; k++) ref[k] = DSB_STACK_PATTERN;
+	} else {
+		for (int k = lo + (int)dsb_lane(); k < hi; k += DSB_WV) ref[k] = DSB_STACK_PATTERN;
+		dsb_wsync();
+	}
+}
+
 #define DSB_S_A_KMER_L 9
 #define DSB_MIN_SCORE_MEM 12
 #define DSB_OVER_SEARCH 50
@@ -958,6 +992,7 @@ DSB_HD void dsb_sc_hash_idx(dsb_read_ws *w)
 /* build_hash_table_M2, src/cly.c:2168-2219: chained 9-mer hash of the read, per strand.
  * Chains keep insertion (= position) order, so heads/tails/next arrays reproduce the
  * reference's lookup order exactly. */
+template <bool WAVE>
 DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 {
 	int both_dir = 0;
@@ -978,18 +1013,60 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 		const dsb_sdir_t *csd = (w->sd[0].direction == direction) ? &w->sd[0] : &w->sd[1];
 		int h = (c_dir == 2) ? 0 : 1;
 		uint32_t *heads = w->hh[h], *tails = w->ht[h], *next = w->hn[h], *kk = w->hk[h];
-		for (uint32_t k = 0; k <= KEY_MASK; k++) heads[k] = 0xffffffffu;
 		const uint8_t *q = w->bin + (csd->strand ? w->L : 0);
-		uint32_t kmer = 0;
-		for (int k = 0; k < DSB_S_A_KMER_L - 1; k++) kmer = (kmer << 2) | q[k];
-		for (uint32_t c_pos = 0; c_pos < (uint32_t)(q_len - DSB_S_A_KMER_L + 1); c_pos++) {
-			kmer = ((kmer << 2) | q[c_pos + DSB_S_A_KMER_L - 1]) & 0x3ffff;
-			uint32_t key = kmer & KEY_MASK;
-			kk[c_pos] = kmer;
-			next[c_pos] = 0xffffffffu;
-			if (heads[key] == 0xffffffffu) heads[key] = c_pos;
-			else next[tails[key]] = c_pos;
-			tails[key] = c_pos;
+		if (!WAVE || (w->dbg & 1)) {
+			for (uint32_t k = 0; k <= KEY_MASK; k++) heads[k] = 0xffffffffu;
+			uint32_t kmer = 0;
+			for (int k = 0; k < DSB_S_A_KMER_L - 1; k++) kmer = (kmer << 2) | q[k];
+			for (uint32_t c_pos = 0; c_pos < (uint32_t)(q_len - DSB_S_A_KMER_L + 1); c_pos++) {
+				kmer = ((kmer << 2) | q[c_pos + DSB_S_A_KMER_L - 1]) & 0x3ffff;
+				uint32_t key = kmer & KEY_MASK;
+				kk[c_pos] = kmer;
+				next[c_pos] = 0xffffffffu;
+				if (heads[key] == 0xffffffffu) heads[key] = c_pos;
+				else next[tails[key]] = c_pos;
+				tails[key] = c_pos;
+			}
+		} else {
+			/* Same lists as the sequential insertion: positions are linked in chunks of 64 in
+			 * position order; inside a chunk each lane finds its same-key neighbours by
+			 * shuffles.  kmer(c) = (OR_k q[c+k] << 2(8-k)) & 0x3ffff is the rolled value. */
+			uint32_t lane = dsb_lane();
+			for (uint32_t k = lane; k <= KEY_MASK; k += DSB_WV) heads[k] = 0xffffffffu;
+			dsb_wsync();
+			uint32_t n_pos = (uint32_t)(q_len - DSB_S_A_KMER_L + 1);
+			for (uint32_t cb = 0; cb < n_pos; cb += DSB_WV) {
+				uint32_t c_pos = cb + lane;
+				int act = c_pos < n_pos;
+				uint32_t kmer = 0;
+				if (act)
+					for (int k = 0; k < DSB_S_A_KMER_L; k++) kmer = (kmer << 2) | q[c_pos + k];
+				kmer &= 0x3ffff;
+				int key = act ? (int)(kmer & KEY_MASK) : -1 - (int)lane;
+				int prev = -1, nxt = -1;
+				for (int o = 0; o < DSB_WV; o++) {
+					int k2 = dsb_wshfl(key, o);
+					if (k2 == key) {
+						if (o < (int)lane) prev = o;
+						else if (o > (int)lane && nxt < 0) nxt = o;
+					}
+				}
+				uint32_t hd = 0, tl = 0;
+				if (act && prev < 0) {
+					hd = heads[key];
+					if (hd != 0xffffffffu) tl = tails[key];
+				}
+				if (act) {
+					kk[c_pos] = kmer;
+					next[c_pos] = (nxt >= 0) ? cb + (uint32_t)nxt : 0xffffffffu;
+					if (prev < 0) {
+						if (hd == 0xffffffffu) heads[key] = c_pos;
+						else next[tl] = c_pos;
+					}
+					if (nxt < 0) tails[key] = c_pos;
+				}
+				dsb_wsync();
+			}
 		}
 	}
 	return key_len;
@@ -1015,10 +1092,14 @@ DSB_HD int dsb_MEM_search(const uint8_t *q, const uint8_t *t, int forward, int m
 	return len;
 }
 
-/* sdp_match, src/cly.c:2330-2435.  q_str: read buffer; t_str: reference window. */
+/* sdp_match, src/cly.c:2330-2435.  q_str: read buffer; t_str: reference window.
+ * WAVE: every 4th window position (the only ones looked up) is one lane; a lane's matches
+ * keep the hash-list order, lanes keep position order (prefix-sum compaction). */
+template <bool WAVE>
 DSB_HDN void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const uint8_t *q_str, const uint8_t *t_str,
 			    uint32_t t_len, int key_len, int hslot, uint32_t t_st, int isForward)
 {
+	if (!WAVE || (w->dbg & 2)) {
 	uint32_t KEY_MASK = (1u << key_len) - 1;
 	uint32_t t_kmer_num = t_len - DSB_S_A_KMER_L + 1;
 	const uint32_t *heads = w->hh[hslot], *next = w->hn[hslot], *kk = w->hk[hslot];
@@ -1086,9 +1167,143 @@ DSB_HDN void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const u
 			}
 		}
 	}
+	} else {
+		uint32_t KEY_MASK = (1u << key_len) - 1;
+		uint32_t t_kmer_num = t_len - DSB_S_A_KMER_L + 1;
+		int lim = (int)t_kmer_num;
+		if (lim <= 4)
+			return;
+		const uint32_t *heads = w->hh[hslot], *next = w->hn[hslot], *kk = w->hk[hslot];
+		int n_i = (lim - 1) >> 2; /* looked-up positions i = 4m, m = 1..n_i */
+		uint32_t lane = dsb_lane();
+		for (int mb = 0; mb < n_i; mb += DSB_WV) {
+			int m = mb + (int)lane + 1;
+			uint32_t cnt = 0;
+			dsb_spd_t e0 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
+			const uint8_t *c_t_str = t_str;
+			uint64_t kmer = 0;
+			int i = 4 * m;
+			if (m <= n_i) {
+				if (isForward) { /* ((k << 2) | c) & 0x3ffff rolled: only the 9 bytes at i remain */
+					c_t_str = t_str + i;
+					for (int k = 0; k < DSB_S_A_KMER_L; k++) kmer = (kmer << 2) | c_t_str[k];
+					kmer &= 0x3ffff;
+				} else {
+					/* (k >> 2) | (c << 16) rolled without a mask: bytes > 3 (pattern/stale window
+					 * bytes, sdp_left's t_offset_global == 0 case) linger for up to 12 steps */
+					c_t_str = t_str + ((int)t_len - DSB_S_A_KMER_L - i);
+					if (i < 16) {
+						const uint8_t *c0 = t_str + ((int)t_len - DSB_S_A_KMER_L - 4);
+						uint64_t k0 = 0;
+						for (int k = 0; k < DSB_S_A_KMER_L; k++) k0 = (k0 << 2) | c0[k];
+						kmer = (k0 << 2) >> (2 * (i - 3));
+					}
+					for (int j = DSB_MAX(4, i - 12); j <= i; j++)
+						kmer |= ((uint64_t)t_str[(int)t_len - DSB_S_A_KMER_L - j] << 16) >> (2 * (i - j));
+				}
+				for (uint32_t nd = heads[kmer & KEY_MASK]; nd != 0xffffffffu; nd = next[nd]) {
+					if (isForward ? (kk[nd] != (uint32_t)kmer) : ((uint64_t)kk[nd] != kmer))
+						continue;
+					uint32_t q_pos = nd;
+					if (!(q_pos >= q_bg && q_pos <= q_ed))
+						continue;
+					dsb_spd_t e;
+					int ok = 0;
+					if (isForward) {
+						int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, 4);
+						if (back_len < 4 || i == 4) {
+							uint32_t max_search = q_ed - q_pos - 1;
+							max_search = DSB_MIN(max_search, t_len - i - 1) + DSB_OVER_SEARCH;
+							int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L,
+											 1, (int)max_search);
+							int total_len = back_len + forward_len + 1;
+							if (total_len >= 4) {
+								e.len = total_len;
+								e.q_pos = q_pos - back_len;
+								e.t_pos = i - back_len + t_st;
+								ok = 1;
+							}
+						}
+					} else {
+						int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L, 1, 4);
+						if (forward_len < 4 || i == 4) {
+							uint32_t max_search = q_pos;
+							max_search = DSB_MIN(max_search, (uint32_t)(c_t_str - t_str)) + DSB_OVER_SEARCH;
+							int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, (int)max_search);
+							int total_len = back_len + forward_len + 1;
+							if (total_len >= 4) {
+								e.len = total_len;
+								e.q_pos = q_pos - back_len;
+								e.t_pos = (uint32_t)(c_t_str - t_str) - back_len + t_st;
+								ok = 1;
+							}
+						}
+					}
+					if (ok) {
+						if (cnt == 0) e0 = e;
+						else if (cnt == 1) e1 = e;
+						cnt++;
+					}
+				}
+			}
+			uint32_t tot, off = dsb_wscan(cnt, &tot);
+			if (tot == 0)
+				continue;
+			if (w->n_sms + tot > w->cap.sms) {
+				w->overflow |= 16;
+				dsb_wsync();
+				return;
+			}
+			dsb_spd_t *dst = w->sms + w->n_sms + off; /* score is left as the buffer holds it */
+			if (cnt > 0) { dst[0].len = e0.len; dst[0].q_pos = e0.q_pos; dst[0].t_pos = e0.t_pos; }
+			if (cnt > 1) { dst[1].len = e1.len; dst[1].q_pos = e1.q_pos; dst[1].t_pos = e1.t_pos; }
+			if (cnt > 2) { /* rare: more than two matches for one position, walk the list again */
+				uint32_t k = 0;
+				for (uint32_t nd = heads[kmer & KEY_MASK]; nd != 0xffffffffu; nd = next[nd]) {
+					if (isForward ? (kk[nd] != (uint32_t)kmer) : ((uint64_t)kk[nd] != kmer))
+						continue;
+					uint32_t q_pos = nd;
+					if (!(q_pos >= q_bg && q_pos <= q_ed))
+						continue;
+					int ok = 0;
+					uint32_t len = 0, qp = 0, tp = 0;
+					if (isForward) {
+						int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, 4);
+						if (back_len < 4 || i == 4) {
+							uint32_t max_search = q_ed - q_pos - 1;
+							max_search = DSB_MIN(max_search, t_len - i - 1) + DSB_OVER_SEARCH;
+							int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L,
+											 1, (int)max_search);
+							int total_len = back_len + forward_len + 1;
+							if (total_len >= 4) { len = total_len; qp = q_pos - back_len; tp = i - back_len + t_st; ok = 1; }
+						}
+					} else {
+						int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L, 1, 4);
+						if (forward_len < 4 || i == 4) {
+							uint32_t max_search = q_pos;
+							max_search = DSB_MIN(max_search, (uint32_t)(c_t_str - t_str)) + DSB_OVER_SEARCH;
+							int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, (int)max_search);
+							int total_len = back_len + forward_len + 1;
+							if (total_len >= 4) {
+								len = total_len; qp = q_pos - back_len;
+								tp = (uint32_t)(c_t_str - t_str) - back_len + t_st; ok = 1;
+							}
+						}
+					}
+					if (ok) {
+						if (k >= 2) { dst[k].len = len; dst[k].q_pos = qp; dst[k].t_pos = tp; }
+						k++;
+					}
+				}
+			}
+			w->n_sms += tot;
+		}
+		dsb_wsync();
+	}
 }
 
 /* sdp_middle_M2, src/cly.c:2439-2525 */
+template <bool WAVE>
 DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, int hslot, int key_len)
 {
 	const dsb_dindex_t *ix = w->ix;
@@ -1118,9 +1333,9 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 					w->overflow |= 32;
 					return 0;
 				}
-				dsb_get_ref_w(w, ref, (uint64_t)(int64_t)(pre_refoffset + pre_mch) + t_offset, (uint32_t)total_ref_len, 1);
-				for (int k = total_ref_len; k < 2000 + 64; k++) ref[k] = DSB_STACK_PATTERN;
-				dsb_sdp_match(w, pre_a->index_in_read + pre_mch - 8, c_a->index_in_read - 1, q_str, ref,
+				dsb_get_ref_win<WAVE>(w, ref, (uint64_t)(int64_t)(pre_refoffset + pre_mch) + t_offset, (uint32_t)total_ref_len);
+				dsb_fill_pattern<WAVE>(ref, total_ref_len, 2000 + 64);
+				dsb_sdp_match<WAVE>(w, pre_a->index_in_read + pre_mch - 8, c_a->index_in_read - 1, q_str, ref,
 					      (uint32_t)total_ref_len, key_len, hslot, (uint32_t)(pre_refoffset + pre_mch), 1);
 				if (w->overflow) return 0;
 			}
@@ -1135,23 +1350,33 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 					int max_score = (int)c_spd->len;
 					uint32_t max_q = c_spd->q_pos + DSB_MAX_SMS_OVERLAP;
 					uint32_t max_t = c_spd->t_pos + DSB_MAX_SMS_OVERLAP;
-					for (int64_t ps = (int64_t)cs - 1; ps >= 0; ps--) {
-						dsb_spd_t *c_pre = w->sms + ps;
-						int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
-						int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
-						if ((uint32_t)pre_q_ed > max_q) continue; /* int vs uint32 */
-						if ((uint32_t)pre_t_ed > max_t) continue;
-						int indel = (int)(c_pre->q_pos - c_pre->t_pos - (max_q - max_t));
-						int ABS_indel = DSB_ABS(indel);
-						if (ABS_indel > 200) continue;
-						int new_score = (int)(c_pre->score + c_spd->len - (uint32_t)(ABS_indel >> 3));
-						if ((uint32_t)pre_q_ed > c_spd->q_pos || (uint32_t)pre_t_ed > c_spd->t_pos) {
-							int overlap_q = pre_q_ed - (int)c_spd->q_pos;
-							int overlap_t = pre_t_ed - (int)c_spd->t_pos;
-							new_score -= DSB_MAX(overlap_q, overlap_t);
+					int best = INT32_MIN;
+					const bool wv = WAVE && !(w->dbg & 4);
+					for (int64_t pb = (int64_t)cs - 1; pb >= 0; pb -= (wv ? DSB_WV : 1)) {
+						int64_t ps = pb - (wv ? (int64_t)dsb_lane() : 0);
+						for (int64_t pe = (wv && ps >= 0) ? ps : 0; ps >= pe; ps--) { /* WAVE: one node per lane */
+							dsb_spd_t *c_pre = w->sms + ps;
+							int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
+							int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
+							if ((uint32_t)pre_q_ed > max_q) continue; /* int vs uint32 */
+							if ((uint32_t)pre_t_ed > max_t) continue;
+							int indel = (int)(c_pre->q_pos - c_pre->t_pos - (max_q - max_t));
+							int ABS_indel = DSB_ABS(indel);
+							if (ABS_indel > 200) continue;
+							int new_score = (int)(c_pre->score + c_spd->len - (uint32_t)(ABS_indel >> 3));
+							if ((uint32_t)pre_q_ed > c_spd->q_pos || (uint32_t)pre_t_ed > c_spd->t_pos) {
+								int overlap_q = pre_q_ed - (int)c_spd->q_pos;
+								int overlap_t = pre_t_ed - (int)c_spd->t_pos;
+								new_score -= DSB_MAX(overlap_q, overlap_t);
+							}
+							best = DSB_MAX(best, new_score);
 						}
-						max_score = DSB_MAX(max_score, new_score);
+						if (!wv)
+							break;
 					}
+					if (wv)
+						best = dsb_wmax(best);
+					max_score = DSB_MAX(max_score, best);
 					score = DSB_MAX(max_score, score);
 					c_spd->score = (uint32_t)max_score;
 				}
@@ -1196,6 +1421,7 @@ DSB_HD int dsb_combine_chain(dsb_read_ws *w, int chain_ID, int dis, int isleft, 
 }
 
 /* sdp_right_M2, src/cly.c:2527-2672 */
+template <bool WAVE>
 DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int key_len, int chain_ID,
 			   uint32_t l_read, int score_ori)
 {
@@ -1207,7 +1433,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 	int32_t combined;
 	w->n_sms = 0;
 	uint8_t *ref = w->win + DSB_WIN_RL; /* uint8_t ref[1000] (src/cly.c:2537) */
-	for (int k = -64; k < 1000 + 64; k++) ref[k] = DSB_STACK_PATTERN; /* ref[-1] is read by sdp_left's back extension */
+	dsb_fill_pattern<WAVE>(ref, -64, 1000 + 64); /* ref[-1] is read by sdp_left's back extension */
 	dsb_spd_t *p = dsb_push_sms(w);
 	if (!p) return 0;
 	p->score = score_ori;
@@ -1233,11 +1459,11 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 			} else
 				max_search_ref = (uint32_t)(t_length - c_t_offset);
 			max_search_ref = DSB_MIN(600u, max_search_ref);
-			dsb_get_ref_w(w, ref, c_t_offset + t_offset_global, max_search_ref + DSB_OVER_SEARCH, 1);
+			dsb_get_ref_win<WAVE>(w, ref, c_t_offset + t_offset_global, max_search_ref + DSB_OVER_SEARCH);
 			int search_q_ed = (int)w->sms[max_sms_id].q_pos + 1000;
 			search_q_ed = DSB_MIN(search_q_ed, l_read);                /* int vs uint32: unsigned */
 			int search_q_st = DSB_MAX(search_q_ed - 2000, c_h->q_st - 8); /* idem (H11) */
-			dsb_sdp_match(w, (uint32_t)search_q_st, (uint32_t)search_q_ed, q_str, ref, max_search_ref, key_len, hslot,
+			dsb_sdp_match<WAVE>(w, (uint32_t)search_q_st, (uint32_t)search_q_ed, q_str, ref, max_search_ref, key_len, hslot,
 				      c_t_offset, 1);
 			if (w->overflow) return 0;
 			c_t_offset += max_search_ref - DSB_S_A_KMER_L - 3;
@@ -1250,29 +1476,70 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 		int max_score = (int)c_sms->len;
 		uint32_t max_pre_q = c_sms->q_pos + DSB_MAX_SMS_OVERLAP;
 		uint32_t max_pre_t = c_sms->t_pos + DSB_MAX_SMS_OVERLAP;
-		for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
-			dsb_spd_t *c_pre = w->sms + ps;
-			int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
-			int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
-			if ((uint32_t)pre_q_ed > max_pre_q) continue; /* int vs uint32 */
-			if ((uint32_t)pre_t_ed > max_pre_t) continue;
-			if (c_pre->t_pos + 600 < max_pre_t) break;
-			int indel = (int)(c_pre->q_pos - c_pre->t_pos - (max_pre_q - max_pre_t));
-			int ABS_indel = DSB_ABS(indel);
-			if (ABS_indel > 200) continue;
-			int new_score = (int)(c_pre->score + c_sms->len - (uint32_t)(ABS_indel >> 3));
-			if ((uint32_t)pre_q_ed > c_sms->q_pos || (uint32_t)pre_t_ed > c_sms->t_pos) {
-				int overlap_q = pre_q_ed - (int)c_sms->q_pos;
-				int overlap_t = pre_t_ed - (int)c_sms->t_pos;
-				new_score -= DSB_MAX(overlap_q, overlap_t);
+		if (!WAVE || (w->dbg & 4)) {
+			for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
+				dsb_spd_t *c_pre = w->sms + ps;
+				int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
+				int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
+				if ((uint32_t)pre_q_ed > max_pre_q) continue; /* int vs uint32 */
+				if ((uint32_t)pre_t_ed > max_pre_t) continue;
+				if (c_pre->t_pos + 600 < max_pre_t) break;
+				int indel = (int)(c_pre->q_pos - c_pre->t_pos - (max_pre_q - max_pre_t));
+				int ABS_indel = DSB_ABS(indel);
+				if (ABS_indel > 200) continue;
+				int new_score = (int)(c_pre->score + c_sms->len - (uint32_t)(ABS_indel >> 3));
+				if ((uint32_t)pre_q_ed > c_sms->q_pos || (uint32_t)pre_t_ed > c_sms->t_pos) {
+					int overlap_q = pre_q_ed - (int)c_sms->q_pos;
+					int overlap_t = pre_t_ed - (int)c_sms->t_pos;
+					new_score -= DSB_MAX(overlap_q, overlap_t);
+				}
+				max_score = DSB_MAX(max_score, new_score);
 			}
-			max_score = DSB_MAX(max_score, new_score);
+		} else { /* lanes scan predecessors downwards; the first `break` node ends the scan */
+			int best = INT32_MIN;
+			uint32_t lane = dsb_lane();
+			for (int64_t pb = (int64_t)current_sms - 2; pb >= 0; pb -= DSB_WV) {
+				int64_t ps = pb - (int64_t)lane;
+				int cand = INT32_MIN, brk = 0;
+				if (ps >= 0) {
+					dsb_spd_t *c_pre = w->sms + ps;
+					int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
+					int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
+					if (!((uint32_t)pre_q_ed > max_pre_q) && !((uint32_t)pre_t_ed > max_pre_t)) {
+						if (c_pre->t_pos + 600 < max_pre_t)
+							brk = 1;
+						else {
+							int indel = (int)(c_pre->q_pos - c_pre->t_pos - (max_pre_q - max_pre_t));
+							int ABS_indel = DSB_ABS(indel);
+							if (ABS_indel <= 200) {
+								cand = (int)(c_pre->score + c_sms->len - (uint32_t)(ABS_indel >> 3));
+								if ((uint32_t)pre_q_ed > c_sms->q_pos || (uint32_t)pre_t_ed > c_sms->t_pos) {
+									int overlap_q = pre_q_ed - (int)c_sms->q_pos;
+									int overlap_t = pre_t_ed - (int)c_sms->t_pos;
+									cand -= DSB_MAX(overlap_q, overlap_t);
+								}
+							}
+						}
+					}
+				}
+				uint64_t bm = dsb_wballot(brk);
+				if (bm) {
+					uint32_t first = (uint32_t)__builtin_ctzll(bm);
+					if (lane >= first)
+						cand = INT32_MIN;
+				}
+				best = DSB_MAX(best, cand);
+				if (bm)
+					break;
+			}
+			best = dsb_wmax(best);
+			max_score = DSB_MAX(max_score, best);
 		}
 		c_sms->score = (uint32_t)max_score;
 		if (c_sms->len >= 8 &&
 		    dsb_combine_chain(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 0, (int)c_sms->q_pos, &combined)) {
 			total_max_score = DSB_MAX(score_ori, max_score) - (int)c_sms->len +
-					  dsb_sdp_middle(w, w->hit[combined].cur, q_str, hslot, key_len);
+					  dsb_sdp_middle<WAVE>(w, w->hit[combined].cur, q_str, hslot, key_len);
 			if (w->overflow) return 0;
 			score_ori = total_max_score;
 			max_sms_id = 0;
@@ -1300,6 +1567,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 }
 
 /* sdp_left_M2, src/cly.c:2674-2814 (the first node's len is not written: H6) */
+template <bool WAVE>
 DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int key_len, int chain_ID,
 			  uint32_t l_read, int score_ori)
 {
@@ -1312,7 +1580,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 	int32_t combined;
 	w->n_sms = 0;
 	uint8_t *ref = w->win + DSB_WIN_RL; /* uint8_t ref[1000] (src/cly.c:2683) */
-	for (int k = -64; k < 1000 + 64; k++) ref[k] = DSB_STACK_PATTERN; /* ref[-1] is read by sdp_left's back extension */
+	dsb_fill_pattern<WAVE>(ref, -64, 1000 + 64); /* ref[-1] is read by sdp_left's back extension */
 	dsb_spd_t *p = dsb_push_sms(w);
 	if (!p) return 0;
 	p->score = score_ori;
@@ -1337,14 +1605,14 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 				max_search_ref = c_t_offset;
 			max_search_ref = DSB_MIN(600u, max_search_ref);
 			if (t_offset_global == 0 && c_t_offset < DSB_OVER_SEARCH + max_search_ref)
-				dsb_get_ref_w(w, ref, c_t_offset + t_offset_global - max_search_ref, max_search_ref, 1);
+				dsb_get_ref_win<WAVE>(w, ref, c_t_offset + t_offset_global - max_search_ref, max_search_ref);
 			else
-				dsb_get_ref_w(w, ref, c_t_offset + t_offset_global - max_search_ref - DSB_OVER_SEARCH,
-					    max_search_ref + DSB_OVER_SEARCH, 1);
+				dsb_get_ref_win<WAVE>(w, ref, c_t_offset + t_offset_global - max_search_ref - DSB_OVER_SEARCH,
+						      max_search_ref + DSB_OVER_SEARCH);
 			int search_q_st = (int)w->sms[max_sms_id].q_pos - 1000;
 			search_q_st = DSB_MAX(search_q_st, 0);
 			int search_q_ed = DSB_MIN(search_q_st + 2000, c_h->q_st - 1); /* int vs uint32: unsigned */
-			dsb_sdp_match(w, (uint32_t)search_q_st, (uint32_t)search_q_ed, q_str, ref + DSB_OVER_SEARCH, max_search_ref,
+			dsb_sdp_match<WAVE>(w, (uint32_t)search_q_st, (uint32_t)search_q_ed, q_str, ref + DSB_OVER_SEARCH, max_search_ref,
 				      key_len, hslot, c_t_offset - max_search_ref, 0);
 			if (w->overflow) return 0;
 			c_t_offset = c_t_offset - max_search_ref + DSB_S_A_KMER_L + 3;
@@ -1357,27 +1625,67 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 		int max_score = (int)c_sms->len;
 		uint32_t min_pre_q = c_sms->q_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
 		uint32_t min_pre_t = c_sms->t_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
-		for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
-			dsb_spd_t *c_pre = w->sms + ps;
-			if (c_pre->q_pos < min_pre_q) continue;
-			if (c_pre->t_pos < min_pre_t) continue;
-			if (min_pre_t + 600 < c_pre->t_pos) break;
-			int indel = (int)(c_pre->q_pos - c_pre->t_pos - (min_pre_q - min_pre_t));
-			int ABS_indel = DSB_ABS(indel);
-			if (ABS_indel > 200) continue;
-			int new_score = (int)(c_pre->score + c_sms->len - (uint32_t)(ABS_indel >> 3));
-			if (min_pre_q + DSB_MAX_SMS_OVERLAP > c_pre->q_pos || min_pre_t + DSB_MAX_SMS_OVERLAP > c_pre->t_pos) {
-				int overlap_q = (int)(min_pre_q + DSB_MAX_SMS_OVERLAP - c_pre->q_pos);
-				int overlap_t = (int)(min_pre_t + DSB_MAX_SMS_OVERLAP - c_pre->t_pos);
-				new_score -= DSB_MAX(overlap_q, overlap_t);
+		if (!WAVE || (w->dbg & 4)) {
+			for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
+				dsb_spd_t *c_pre = w->sms + ps;
+				if (c_pre->q_pos < min_pre_q) continue;
+				if (c_pre->t_pos < min_pre_t) continue;
+				if (min_pre_t + 600 < c_pre->t_pos) break;
+				int indel = (int)(c_pre->q_pos - c_pre->t_pos - (min_pre_q - min_pre_t));
+				int ABS_indel = DSB_ABS(indel);
+				if (ABS_indel > 200) continue;
+				int new_score = (int)(c_pre->score + c_sms->len - (uint32_t)(ABS_indel >> 3));
+				if (min_pre_q + DSB_MAX_SMS_OVERLAP > c_pre->q_pos || min_pre_t + DSB_MAX_SMS_OVERLAP > c_pre->t_pos) {
+					int overlap_q = (int)(min_pre_q + DSB_MAX_SMS_OVERLAP - c_pre->q_pos);
+					int overlap_t = (int)(min_pre_t + DSB_MAX_SMS_OVERLAP - c_pre->t_pos);
+					new_score -= DSB_MAX(overlap_q, overlap_t);
+				}
+				max_score = DSB_MAX(max_score, new_score);
 			}
-			max_score = DSB_MAX(max_score, new_score);
+		} else {
+			int best = INT32_MIN;
+			uint32_t lane = dsb_lane();
+			for (int64_t pb = (int64_t)current_sms - 2; pb >= 0; pb -= DSB_WV) {
+				int64_t ps = pb - (int64_t)lane;
+				int cand = INT32_MIN, brk = 0;
+				if (ps >= 0) {
+					dsb_spd_t *c_pre = w->sms + ps;
+					if (!(c_pre->q_pos < min_pre_q) && !(c_pre->t_pos < min_pre_t)) {
+						if (min_pre_t + 600 < c_pre->t_pos)
+							brk = 1;
+						else {
+							int indel = (int)(c_pre->q_pos - c_pre->t_pos - (min_pre_q - min_pre_t));
+							int ABS_indel = DSB_ABS(indel);
+							if (ABS_indel <= 200) {
+								cand = (int)(c_pre->score + c_sms->len - (uint32_t)(ABS_indel >> 3));
+								if (min_pre_q + DSB_MAX_SMS_OVERLAP > c_pre->q_pos ||
+								    min_pre_t + DSB_MAX_SMS_OVERLAP > c_pre->t_pos) {
+									int overlap_q = (int)(min_pre_q + DSB_MAX_SMS_OVERLAP - c_pre->q_pos);
+									int overlap_t = (int)(min_pre_t + DSB_MAX_SMS_OVERLAP - c_pre->t_pos);
+									cand -= DSB_MAX(overlap_q, overlap_t);
+								}
+							}
+						}
+					}
+				}
+				uint64_t bm = dsb_wballot(brk);
+				if (bm) {
+					uint32_t first = (uint32_t)__builtin_ctzll(bm);
+					if (lane >= first)
+						cand = INT32_MIN;
+				}
+				best = DSB_MAX(best, cand);
+				if (bm)
+					break;
+			}
+			best = dsb_wmax(best);
+			max_score = DSB_MAX(max_score, best);
 		}
 		c_sms->score = (uint32_t)max_score;
 		if (c_sms->len >= 8 && dsb_combine_chain(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 1,
 							 (int)(c_sms->q_pos + c_sms->len), &combined)) {
 			total_max_score = DSB_MAX(score_ori, max_score) - (int)c_sms->len +
-					  dsb_sdp_middle(w, w->hit[combined].cur, q_str, hslot, key_len);
+					  dsb_sdp_middle<WAVE>(w, w->hit[combined].cur, q_str, hslot, key_len);
 			if (w->overflow) return 0;
 			score_ori = total_max_score;
 			max_sms_id = 0;
@@ -1404,20 +1712,21 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 }
 
 /* get_score_M2, src/cly.c:2816-2844 */
+template <bool WAVE>
 DSB_HDN void dsb_get_score(dsb_read_ws *w, uint32_t l_read)
 {
-	int key_len = dsb_build_hash_table(w, (int)l_read);
+	int key_len = dsb_build_hash_table<WAVE>(w, (int)l_read);
 	for (uint32_t i = 0; i < w->n_hit; i++) {
 		if (w->hit[i].sum_score == 0)
 			continue;
 		const dsb_sdir_t *csd = (w->sd[0].direction == w->hit[i].direction) ? &w->sd[0] : &w->sd[1];
 		int hslot = (w->hit[i].direction == DSB_FORWARD) ? 0 : 1;
 		const uint8_t *q_str = w->bin + (csd->strand ? w->L : 0);
-		int score = dsb_sdp_middle(w, w->hit[i].cur, q_str, hslot, key_len);
+		int score = dsb_sdp_middle<WAVE>(w, w->hit[i].cur, q_str, hslot, key_len);
 		if (w->overflow) return;
-		score = dsb_sdp_right(w, q_str, hslot, key_len, (int)i, l_read, score);
+		score = dsb_sdp_right<WAVE>(w, q_str, hslot, key_len, (int)i, l_read, score);
 		if (w->overflow) return;
-		score = dsb_sdp_left(w, q_str, hslot, key_len, (int)i, l_read, score);
+		score = dsb_sdp_left<WAVE>(w, q_str, hslot, key_len, (int)i, l_read, score);
 		if (w->overflow) return;
 		w->hit[i].sum_score = (uint32_t)score;
 	}
@@ -1448,6 +1757,7 @@ DSB_HD int dsb_chain_cmp_by_MEM_score(const dsb_chain_t *a, const dsb_chain_t *b
 }
 
 /* delete_small_score_rst, src/cly.c:2878-2952 — part A (up to the max_read_l update) */
+template <bool WAVE>
 DSB_HDN void dsb_delete_small_A(dsb_read_ws *w)
 {
 	w->reached_update = 0;
@@ -1461,7 +1771,7 @@ DSB_HDN void dsb_delete_small_A(dsb_read_ws *w)
 	w->n_hit = DSB_MIN(400u, w->n_hit);
 	uint32_t l_read = w->L;
 	dsb_sc_hash_idx(w);
-	dsb_get_score(w, l_read);
+	dsb_get_score<WAVE>(w, l_read);
 	if (w->overflow)
 		return;
 	uint32_t n = w->n_hit;
@@ -1593,48 +1903,143 @@ DSB_HDN void dsb_detect_primary(dsb_read_ws *w, uint32_t read_len, int *primary_
 	}
 }
 
-/* classify_seq, src/cly.c:3059-3127 — part A: everything before the max_read_l update. */
+/*
+ * classify_seq, src/cly.c:3059-3127 — part A (everything before the max_read_l update),
+ * cut into phases so that each can run as its own launch over all reads of a chunk.
+ * dsb_rflags_t carries the control decisions between phases; running the phases in order
+ * is exactly the reference's control flow (including the returns on overflow).
+ */
+enum {
+	DSB_PH_ISLAND = 0, /* get_island: seed vectors of both strands */
+	DSB_PH_FAST0,      /* fast_classify, forward seed vector */
+	DSB_PH_FAST1,      /* fast_classify, reverse seed vector (both_direction) */
+	DSB_PH_RESOLVE_F,  /* resolve_tree (chaining + SDP), slow-mode decision */
+	DSB_PH_SLOW0,      /* slow_classify, forward */
+	DSB_PH_RESOLVE_S0,
+	DSB_PH_SLOW1,      /* slow_classify, reverse */
+	DSB_PH_RESOLVE_S1,
+	DSB_PH_DELA,       /* delete_small_score_rst part A */
+	DSB_PH_N
+};
+
+typedef struct {
+	uint8_t done;      /* read finished early (short read / overflow) */
+	uint8_t both;      /* both_direction */
+	uint8_t run_slow;
+	uint8_t slow1;
+} dsb_rflags_t;
+
+/* does phase ph do any work for this read? (lets the host skip empty launches) */
+DSB_HD int dsb_phase_active(const dsb_read_ws *w, const dsb_rflags_t *f, int ph)
+{
+	if (ph == DSB_PH_ISLAND)
+		return 1;
+	if (f->done || w->overflow)
+		return 0;
+	switch (ph) {
+	case DSB_PH_FAST1: return f->both;
+	case DSB_PH_SLOW0: case DSB_PH_RESOLVE_S0: return f->run_slow;
+	case DSB_PH_SLOW1: case DSB_PH_RESOLVE_S1: return f->run_slow && f->slow1;
+	default: return 1;
+	}
+}
+
+DSB_HD void dsb_phase(dsb_read_ws *w, dsb_rflags_t *f, int ph)
+{
+	if (!dsb_phase_active(w, f, ph))
+		return;
+	const int super_repeat = 0; /* fast_classify returns super_repeat[0], never incremented */
+	switch (ph) {
+	case DSB_PH_ISLAND:
+		w->n_anc = 0;
+		w->fast_classify = 1;
+		w->n_hit = 0;
+		w->reached_update = 0;
+		f->done = f->both = f->run_slow = f->slow1 = 0;
+		if (w->L < DSB_MIN_READ_LEN) {
+			f->done = 1;
+			return;
+		}
+		dsb_get_island(w);
+		f->both = ((w->sd[0].total_score - w->sd[1].total_score) <= (w->sd[0].total_score >> 3));
+		return;
+	case DSB_PH_FAST0:
+		dsb_fast_classify(w, &w->sd[0]);
+		return;
+	case DSB_PH_FAST1:
+		dsb_fast_classify(w, &w->sd[1]);
+		return;
+	case DSB_PH_RESOLVE_F:
+		dsb_resolve_tree(w);
+		if (w->overflow)
+			return;
+		if (w->n_hit <= 0)
+			f->run_slow = 1;
+		else if (w->hit[0].anchor_number < 5 && super_repeat < 3) {
+			f->run_slow = 1;
+			if (w->L <= 300 && w->hit[0].sum_score > 200)
+				f->run_slow = 0;
+		}
+		if (f->run_slow)
+			w->n_anc = 0;
+		return;
+	case DSB_PH_SLOW0:
+		dsb_slow_classify(w, &w->sd[0]);
+		return;
+	case DSB_PH_RESOLVE_S0:
+		dsb_resolve_tree(w);
+		if (w->overflow)
+			return;
+		f->slow1 = (f->both || w->n_hit <= 0 || (w->hit[0].anchor_number < 5 && super_repeat < 3));
+		return;
+	case DSB_PH_SLOW1:
+		dsb_slow_classify(w, &w->sd[1]);
+		return;
+	case DSB_PH_RESOLVE_S1:
+		dsb_resolve_tree(w);
+		return;
+	case DSB_PH_DELA:
+		dsb_delete_small_A<false>(w);
+		return;
+	}
+}
+
 DSB_HDN void dsb_classify_A(dsb_read_ws *w)
 {
-	w->n_anc = 0;
-	w->fast_classify = 1;
-	w->n_hit = 0;
-	w->reached_update = 0;
-	if (w->L < DSB_MIN_READ_LEN)
-		return;
-	dsb_get_island(w);
-	int both_direction = ((w->sd[0].total_score - w->sd[1].total_score) <= (w->sd[0].total_score >> 3));
-	int super_repeat = 0; /* fast_classify returns super_repeat[0], never incremented */
-	dsb_fast_classify(w, &w->sd[0]);
-	if (w->overflow) return;
-	if (both_direction) {
-		dsb_fast_classify(w, &w->sd[1]);
-		if (w->overflow) return;
-	}
-	dsb_resolve_tree(w);
-	if (w->overflow) return;
-	int run_slow_mode = 0;
-	if (w->n_hit <= 0)
-		run_slow_mode = 1;
-	else if (w->hit[0].anchor_number < 5 && super_repeat < 3) {
-		run_slow_mode = 1;
-		if (w->L <= 300 && w->hit[0].sum_score > 200)
-			run_slow_mode = 0;
-	}
-	if (run_slow_mode) {
-		w->n_anc = 0;
-		dsb_slow_classify(w, &w->sd[0]);
-		if (w->overflow) return;
-		dsb_resolve_tree(w);
-		if (w->overflow) return;
-		if (both_direction || w->n_hit <= 0 || (w->hit[0].anchor_number < 5 && super_repeat < 3)) {
-			dsb_slow_classify(w, &w->sd[1]);
-			if (w->overflow) return;
-			dsb_resolve_tree(w);
-			if (w->overflow) return;
-		}
-	}
-	dsb_delete_small_A(w);
+	dsb_rflags_t f = {0, 0, 0, 0};
+	for (int ph = 0; ph < DSB_PH_N; ph++)
+		dsb_phase(w, &f, ph);
+}
+
+/* Per-read state carried between phase launches (in the read's workspace). */
+typedef struct {
+	dsb_sdir_t sd[2];
+	uint32_t n_anc, n_hit, fast_classify, overflow, reached_update;
+	dsb_rflags_t f;
+} dsb_rstate_t;
+
+DSB_HD void dsb_state_save(const dsb_read_ws *w, const dsb_rflags_t *f, dsb_rstate_t *s)
+{
+	s->sd[0] = w->sd[0];
+	s->sd[1] = w->sd[1];
+	s->n_anc = w->n_anc;
+	s->n_hit = w->n_hit;
+	s->fast_classify = w->fast_classify;
+	s->overflow = w->overflow;
+	s->reached_update = w->reached_update;
+	s->f = *f;
+}
+
+DSB_HD void dsb_state_load(dsb_read_ws *w, dsb_rflags_t *f, const dsb_rstate_t *s)
+{
+	w->sd[0] = s->sd[0];
+	w->sd[1] = s->sd[1];
+	w->n_anc = s->n_anc;
+	w->n_hit = s->n_hit;
+	w->fast_classify = s->fast_classify;
+	w->overflow = s->overflow;
+	w->reached_update = s->reached_update;
+	*f = s->f;
 }
 
 

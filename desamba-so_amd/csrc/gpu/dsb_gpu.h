@@ -21,6 +21,7 @@ typedef struct {
 	double ms_total;      /* wall time of dsb_gpu_classify, host-measured */
 	double ms_h2d, ms_d2h;
 	double ms_encode, ms_seed, ms_classA, ms_classB; /* HIP-event kernel times, summed over chunks */
+	double ms_phase[12];  /* k_phase<ph> times (ms_classA = their sum) */
 	uint64_t n_reads, n_bases, n_retry, n_chunks;
 	uint64_t seed_positions; /* k-mer positions probed by the seed kernel (both strands) */
 	uint64_t stats[DSB_N_STATS]; /* work counters (DSB_ST_*): [0,16) k_classA, [16,32) k_classB */

@@ -12,6 +12,7 @@
 
 #define DSB_BIN_GUARD 64   /* bytes before F: the last 8 = glibc chunk header of the reference buffer */
 #define DSB_BIN_TAIL 256   /* bytes after R, MALLOC_PERTURB fill */
+#define DSB_STATE_BYTES 128
 #define DSB_CAP_RETRY 8
 
 DSB_HD uint64_t dsb_al(uint64_t x) { return (x + 255) & ~255ull; }
@@ -64,7 +65,7 @@ DSB_HD dsb_ws_layout dsb_layout(uint32_t L, dsb_caps_t cap)
 	o.win = p; p = dsb_al(p + DSB_WIN_BYTES);
 	o.mem = p; p = dsb_al(p + sizeof(dsb_mem_t) * 256);
 	o.spset = p; p = dsb_al(p + 8 * 512);
-	o.state = p; p = dsb_al(p + 2 * sizeof(dsb_sdir_t)); /* SEARCH_DIR pair kept for diagnostics */
+	o.state = p; p = dsb_al(p + DSB_STATE_BYTES); /* dsb_rstate_t: state between phase launches */
 	o.total = p;
 	return o;
 }
@@ -107,6 +108,7 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 	w->max_read_l = 0;
 	w->reached_update = 0;
 	w->stats = 0;
+	w->dbg = 0;
 }
 
 /* glibc chunk-size word in front of the reference's bin_read = realloc(NULL, 2L+20)

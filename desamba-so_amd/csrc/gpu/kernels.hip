@@ -103,45 +103,104 @@ __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ i
 		ex[word] = bits;
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(64) void k_classA(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
-						const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
-						uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
-						dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
-						unsigned long long *__restrict__ gstats)
+static_assert(sizeof(dsb_rstate_t) <= DSB_STATE_BYTES, "per-read phase state must fit its workspace slot");
+
+/* One phase of classify part A (dsb_phase), one lane per read; the read's control state
+ * lives in its workspace between launches.  The last phase publishes the read's summary. */
+template <int PH, bool STATS>
+__global__ __launch_bounds__(64) void k_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+					       const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+					       uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+					       dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
+					       unsigned long long *__restrict__ gstats)
 {
 	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= n)
 		return;
 	uint32_t r = order[t];
 	uint32_t L = len[r];
+	uint8_t *base = ws + ws_off[r];
+	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
 	dsb_read_ws w;
-	dsb_ws_init(&w, ix, ws + ws_off[r], L, dsb_default_caps(L, scale[r]));
+	dsb_ws_init(&w, ix, base, L, cap);
+	dsb_rstate_t *sp = (dsb_rstate_t *)(base + dsb_layout(L, cap).state);
+	dsb_rflags_t f = {0, 0, 0, 0};
+	if (PH != DSB_PH_ISLAND)
+		dsb_state_load(&w, &f, sp);
 	uint64_t st[DSB_ST_N];
 	if (STATS) {
 		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
 		w.stats = st;
 	}
-	dsb_classify_A(&w);
-	{
-		dsb_sdir_t *sv = (dsb_sdir_t *)(ws + ws_off[r] + dsb_layout(L, w.cap).state);
-		sv[0] = w.sd[0];
-		sv[1] = w.sd[1];
+	dsb_phase(&w, &f, PH);
+	dsb_state_save(&w, &f, sp);
+	if (PH == DSB_PH_DELA) {
+		dsb_read_out_t o;
+		o.n_hit = w.n_hit;
+		o.n_anchor = w.n_anc;
+		o.fast = w.fast_classify;
+		o.status = w.overflow;
+		o.reached_update = w.reached_update;
+		o.pad = 0;
+		o.hit_off = 0;
+		ro[r] = o;
+		if (w.overflow)
+			atomicAdd(n_overflow, 1u);
 	}
-	dsb_read_out_t o;
-	o.n_hit = w.n_hit;
-	o.n_anchor = w.n_anc;
-	o.fast = w.fast_classify;
-	o.status = w.overflow;
-	o.reached_update = w.reached_update;
-	o.pad = 0;
-	o.hit_off = 0;
-	ro[r] = o;
-	if (w.overflow)
-		atomicAdd(n_overflow, 1u);
-	if (STATS && !w.overflow)
+	if (STATS)
 		for (int k = 0; k < DSB_ST_N; k++)
 			atomicAdd(gstats + k, (unsigned long long)st[k]);
+}
+
+/* The last phase of part A (delete_small_score_rst A: read hash, sparse-DP scoring of every
+ * chain, merge) with one wavefront per read (dsb_wave.h); one wave per workgroup. */
+template <bool STATS>
+__global__ __launch_bounds__(64) void k_delA_wave(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+						   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+						   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+						   dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
+						   unsigned long long *__restrict__ gstats, uint32_t dbg)
+{
+	uint32_t t = blockIdx.x;
+	if (t >= n)
+		return;
+	uint32_t lane = threadIdx.x;
+	uint32_t r = order[t];
+	uint32_t L = len[r];
+	uint8_t *base = ws + ws_off[r];
+	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
+	dsb_read_ws w;
+	dsb_ws_init(&w, ix, base, L, cap);
+	dsb_rstate_t *sp = (dsb_rstate_t *)(base + dsb_layout(L, cap).state);
+	dsb_rflags_t f;
+	dsb_state_load(&w, &f, sp);
+	w.dbg = dbg;
+	uint64_t st[DSB_ST_N];
+	if (STATS) {
+		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
+		w.stats = st;
+	}
+	if (dsb_phase_active(&w, &f, DSB_PH_DELA))
+		dsb_delete_small_A<true>(&w);
+	__syncthreads();
+	if (lane == 0) {
+		dsb_state_save(&w, &f, sp);
+		dsb_read_out_t o;
+		o.n_hit = w.n_hit;
+		o.n_anchor = w.n_anc;
+		o.fast = w.fast_classify;
+		o.status = w.overflow;
+		o.reached_update = w.reached_update;
+		o.pad = 0;
+		o.hit_off = 0;
+		ro[r] = o;
+		if (w.overflow)
+			atomicAdd(n_overflow, 1u);
+	}
+	if (STATS)
+		for (int k = 0; k < DSB_ST_N; k++)
+			if (st[k])
+				atomicAdd(gstats + k, (unsigned long long)st[k]);
 }
 
 template <bool STATS>
@@ -378,6 +437,29 @@ static double now_ms(void)
 	return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
 }
 
+typedef void (*phase_kernel_t)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
+			       const uint32_t *, uint32_t, dsb_read_out_t *, uint32_t *, unsigned long long *);
+template <int PH>
+static phase_kernel_t phase_kernel(bool stats)
+{
+	return stats ? k_phase<PH, true> : k_phase<PH, false>;
+}
+static phase_kernel_t phase_kernel_at(int ph, bool stats)
+{
+	switch (ph) {
+	case 0: return phase_kernel<0>(stats);
+	case 1: return phase_kernel<1>(stats);
+	case 2: return phase_kernel<2>(stats);
+	case 3: return phase_kernel<3>(stats);
+	case 4: return phase_kernel<4>(stats);
+	case 5: return phase_kernel<5>(stats);
+	case 6: return phase_kernel<6>(stats);
+	case 7: return phase_kernel<7>(stats);
+	default: return phase_kernel<8>(stats);
+	}
+}
+static_assert(DSB_PH_N == 9, "phase dispatch table");
+
 static float ev_ms(dsb_gpu_dev *g)
 {
 	hipEventRecord(g->ev_b, g->stream);
@@ -418,6 +500,28 @@ static uint64_t seed_words(const std::vector<uint32_t> &len, uint64_t cb, const 
 	}
 	off[m] = tw;
 	return tw;
+}
+
+static uint32_t wave_dbg(void)
+{
+	const char *e = getenv("DSB_WAVE_DBG");
+	return e ? (uint32_t)strtoul(e, NULL, 0) : 0;
+}
+
+/* one phase of part A over the reads order[0..m): lane-per-read kernels, except the
+ * scoring phase (one wavefront per read) */
+static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl, uint8_t *wsb, const uint32_t *order,
+			 uint32_t m)
+{
+	hipStream_t s = g->stream;
+	if (ph == DSB_PH_DELA)
+		hipLaunchKernelGGL(stats ? k_delA_wave<true> : k_delA_wave<false>, dim3(m), dim3(64), 0, s, g->d, cl,
+				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
+				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), wave_dbg());
+	else
+		hipLaunchKernelGGL(phase_kernel_at(ph, stats), dim3((m + 63) / 64), dim3(64), 0, s, g->d, cl,
+				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
+				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>());
 }
 
 /* a batch of reads resident in HBM (sequences only) + its results */
@@ -532,16 +636,14 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			HIP_OK(hipGetLastError());
 		}
 		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
-		hipEventRecord(g->ev_a, s);
-		if (stats_on)
-			k_classA<true><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
-								     g->order.as<uint32_t>(), cn, g->ro.as<dsb_read_out_t>(),
-								     g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>());
-		else
-			k_classA<false><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
-								      g->order.as<uint32_t>(), cn, g->ro.as<dsb_read_out_t>(),
-								      g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>());
-		T.ms_classA += ev_ms(g);
+		for (int ph = 0; ph < DSB_PH_N; ph++) {
+			hipEventRecord(g->ev_a, s);
+			launch_phase(g, ph, stats_on != 0, cl, wsb, g->order.as<uint32_t>(), cn);
+			float ms = ev_ms(g);
+			T.ms_phase[ph] += ms;
+			T.ms_classA += ms;
+			HIP_OK(hipGetLastError());
+		}
 		HIP_OK(hipGetLastError());
 		uint32_t n_over = 0;
 		HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
@@ -588,9 +690,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				k_seed<<<(uint32_t)((tw2 * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
 											      g->wo2.as<uint64_t>(), g->sel.as<uint32_t>(), m, tw2);
 			HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
-			k_classA<false><<<(m + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
-								     g->sel.as<uint32_t>(), m, g->ro.as<dsb_read_out_t>(),
-								     g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>());
+			for (int ph = 0; ph < DSB_PH_N; ph++)
+				launch_phase(g, ph, false, cl, wsb, g->sel.as<uint32_t>(), m);
 			HIP_OK(hipGetLastError());
 			HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
 			HIP_OK(hipMemcpy(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));

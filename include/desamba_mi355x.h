@@ -16,6 +16,7 @@ typedef struct {
 	double ms_total;       /* host wall time of the GPU classify call */
 	double ms_h2d, ms_d2h; /* read upload / result download (host-measured) */
 	double ms_encode, ms_seed, ms_classA, ms_classB; /* per-kernel HIP-event times */
+	double ms_phase[12];   /* classify part A per phase (island, fast0/1, resolve, slow0/1, ...) */
 	uint64_t n_reads, n_bases, n_retry, n_chunks;
 	uint64_t seed_positions; /* k-mer positions probed by k_seed (both strands) */
 	uint64_t stats[32];    /* work counters: [0,16) k_classA, [16,32) k_classB */

@@ -90,7 +90,12 @@ int main(int argc, char **argv)
 					}
 				}
 			}
-			dsb_classify_A(&w);
+			if (getenv("EMU_WAVE")) { /* the wave-cooperative code paths, as a one-lane wave */
+				dsb_rflags_t f = {0, 0, 0, 0};
+				for (int ph = 0; ph < DSB_PH_DELA; ph++) dsb_phase(&w, &f, ph);
+				if (dsb_phase_active(&w, &f, DSB_PH_DELA)) dsb_delete_small_A<true>(&w);
+			} else
+				dsb_classify_A(&w);
 			if (getenv("DSB_DEBUG_READ") && strtoull(getenv("DSB_DEBUG_READ"), 0, 10) == i)
 				dsb_debug_dump(stderr, &w, "emuA");
 			if (w.overflow) {
