@@ -257,9 +257,47 @@ DSB_HD int dsb_spset_insert(uint64_t node, dsb_spset_t *s)
 	return 1;
 }
 
+DSB_HD void dsb_set_reset(dsb_spset_t *s) { s->l = 0; }
+DSB_HD int dsb_set_insert(uint64_t node, dsb_spset_t *s) { return dsb_spset_insert(node, s); }
+
+/*
+ * The same set as an open-addressing hash (one per lane of the wave-cooperative seeding):
+ * membership == "inserted since the last reset or since the last wrap of the reference's
+ * 500-entry array" (a wrap is `l == m -> l = 0`, i.e. the array forgets everything), so a
+ * generation counter replaces clearing.  Slot = gen << 40 | node (BWT rows < 2^40), 0 = empty.
+ */
+#define DSB_HSET_SLOTS 1024
+typedef struct { uint64_t *tab; uint32_t stride, gen; int l, m; } dsb_hset_t;
+DSB_HD void dsb_set_reset(dsb_hset_t *s)
+{
+	s->l = 0;
+	s->gen++;
+}
+DSB_HD int dsb_set_insert(uint64_t node, dsb_hset_t *s)
+{
+	if (s->l == s->m) {
+		s->l = 0;
+		s->gen++;
+	}
+	uint32_t h = (uint32_t)((node * 0x9E3779B97F4A7C15ull) >> 54);
+	uint64_t key = ((uint64_t)s->gen << 40) | node;
+	for (;;) {
+		uint64_t v = s->tab[(uint64_t)h * s->stride];
+		if (v == key)
+			return 0;
+		if ((uint32_t)(v >> 40) != s->gen) {
+			s->tab[(uint64_t)h * s->stride] = key;
+			s->l++;
+			return 1;
+		}
+		h = (h + 1) & (DSB_HSET_SLOTS - 1);
+	}
+}
+
 /* bwt_single_search, src/cly.c:1339-1378; `string` indexes the read buffer, read backwards */
+template <typename SET>
 DSB_HD void dsb_single_search(dsb_read_ws *w, uint64_t sp, const uint8_t *string, int max_match_len,
-			       dsb_spset_t *sp_set, dsb_mem_t *mem_rst)
+			       SET *sp_set, dsb_mem_t *mem_rst)
 {
 	const dsb_dindex_t *ix = w->ix;
 	uint64_t new_sp, sa_sp = ~0ull;
@@ -278,7 +316,7 @@ DSB_HD void dsb_single_search(dsb_read_ws *w, uint64_t sp, const uint8_t *string
 			break;
 		match_len++;
 		string--;
-		if (dsb_spset_insert(new_sp, sp_set) == 0) {
+		if (dsb_set_insert(new_sp, sp_set) == 0) {
 			mem_rst->match_len = -1000;
 			return;
 		}
@@ -291,8 +329,9 @@ DSB_HD void dsb_single_search(dsb_read_ws *w, uint64_t sp, const uint8_t *string
 }
 
 /* bwt_MEM_search, src/cly.c:1383-1442 */
+template <typename SET>
 DSB_HD int dsb_mem_search(dsb_read_ws *w, const uint8_t *string, uint64_t pre_v, int max_rst, int l_min_mth,
-			   int l_max_mth, dsb_spset_t *sp_set, dsb_mem_t *mem_rst)
+			   int l_max_mth, SET *sp_set, dsb_mem_t *mem_rst)
 {
 	const dsb_dindex_t *ix = w->ix;
 	int n_rst = 0;
@@ -322,7 +361,7 @@ DSB_HD int dsb_mem_search(dsb_read_ws *w, const uint8_t *string, uint64_t pre_v,
 	if (new_sp >= new_ep)
 		return 0;
 	if (new_sp + 1 == new_ep) {
-		if (dsb_spset_insert(new_sp, sp_set) == 0)
+		if (dsb_set_insert(new_sp, sp_set) == 0)
 			return 0;
 		dsb_single_search(w, new_sp, string, DSB_MAX(0, l_max_mth - match_len), sp_set, mem_rst + n_rst);
 		mem_rst[n_rst].match_len += match_len + 1;
@@ -330,7 +369,7 @@ DSB_HD int dsb_mem_search(dsb_read_ws *w, const uint8_t *string, uint64_t pre_v,
 			n_rst++;
 	} else {
 		for (uint64_t c_sp = new_sp; c_sp < new_ep; c_sp++) {
-			if (dsb_spset_insert(c_sp, sp_set) == 0)
+			if (dsb_set_insert(c_sp, sp_set) == 0)
 				continue;
 			dsb_single_search(w, c_sp, string, DSB_MAX(0, l_max_mth - match_len), sp_set, mem_rst + n_rst);
 			mem_rst[n_rst].match_len += match_len + 1;
@@ -606,58 +645,169 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 /* ------------------------------------------------------------------ fast / slow */
 #define DSB_MEM_SEARCH_FAST 2
 #define DSB_MIN_MEM_LEN_FAST 21
-/* fast_classify, src/cly.c:1473-1541 */
-DSB_HDN void dsb_fast_classify(dsb_read_ws *w, const dsb_sdir_t *s_d)
+/* One seed of fast_classify (src/cly.c:1483-1538): FM searches along the seed, map_seed of
+ * the hits (anchors pushed at w->n_anc), then the seed's anchors below its top score are
+ * marked useless.  Returns 1 when the reference skips the next seed (`ci++`). */
+template <typename SET>
+DSB_HD int dsb_fast_seed(dsb_read_ws *w, const dsb_sdir_t *s_d, uint32_t ci, SET *sp_set)
 {
 	const dsb_dindex_t *ix = w->ix;
 	uint8_t l_ek = (uint8_t)ix->l_ek;
 	int min_index = DSB_MIN_MEM_LEN_FAST - l_ek;
 	uint8_t *bin_read = w->bin + (s_d->strand ? w->L : 0);
-	dsb_spset_t sp_set = {w->spset, 0, 500};
 	dsb_mem_t m_r[DSB_MEM_SEARCH_FAST];
-	dsb_seed_t *sv_b = w->seeds + s_d->seed_off;
-	uint32_t n_sv = s_d->l_seed_v_f;
-	dsb_seedinfo_t s_i = {bin_read, w->L, 0, s_d->direction};
-	for (uint32_t ci = 0; ci < n_sv; ci++) {
-		dsb_seed_t *c_sv = sv_b + ci;
-		if (c_sv->top == 0)
+	dsb_seed_t *c_sv = w->seeds + s_d->seed_off + ci;
+	dsb_seedinfo_t s_i = {bin_read, w->L, (uint16_t)ci, s_d->direction};
+	dsb_set_reset(sp_set);
+	uint32_t a_b_idx = w->n_anc;
+	int skip = 0;
+	for (int j = (int)c_sv->len - 1; j >= min_index;) {
+		int kmer_index = (int)c_sv->offset + j;
+		uint64_t kmer = dsb_kmer_at(bin_read + kmer_index, l_ek, ix->single_base_max);
+		uint64_t prefixValue = kmer & DSB_PRE_IDX_MASK;
+		int string_index = kmer_index + l_ek - 1;
+		int n_m = dsb_mem_search(w, bin_read + string_index, prefixValue, DSB_MEM_SEARCH_FAST,
+					 DSB_MIN_MEM_LEN_FAST - 1, string_index, sp_set, m_r);
+		if (n_m == 0) {
+			j -= 2;
 			continue;
-		sp_set.l = 0;
-		s_i.seed_ID = (uint16_t)ci;
-		uint32_t a_b_idx = w->n_anc;
-		for (int j = (int)c_sv->len - 1; j >= min_index;) {
-			int kmer_index = (int)c_sv->offset + j;
-			uint64_t kmer = dsb_kmer_at(bin_read + kmer_index, l_ek, ix->single_base_max);
-			uint64_t prefixValue = kmer & DSB_PRE_IDX_MASK;
-			int string_index = kmer_index + l_ek - 1;
-			int n_m = dsb_mem_search(w, bin_read + string_index, prefixValue, DSB_MEM_SEARCH_FAST,
-						 DSB_MIN_MEM_LEN_FAST - 1, string_index, &sp_set, m_r);
-			if (n_m == 0) {
-				j -= 2;
-				continue;
-			}
-			j -= 3;
-			int max_score = 0;
-			for (int k = 0; k < n_m; k++) {
-				m_r[k].read_offset = string_index - m_r[k].match_len;
-				int c_score = dsb_map_seed(w, m_r + k, &s_i);
-				max_score = DSB_MAX(c_score, max_score);
-			}
-			if (w->overflow)
-				return;
-			if (max_score > 35)
-				j -= 7;
-			if (max_score > 256) {
-				if (max_score > 512)
-					ci++;
-				break;
-			}
 		}
-		int top_score = 35;
-		for (uint32_t k = a_b_idx; k < w->n_anc; k++)
-			top_score = DSB_MAX(top_score, (int)w->anc[k].score);
-		for (uint32_t k = a_b_idx; k < w->n_anc; k++)
-			w->anc[k].anchor_useless = (w->anc[k].score < top_score) ? 1 : 0;
+		j -= 3;
+		int max_score = 0;
+		for (int k = 0; k < n_m; k++) {
+			m_r[k].read_offset = string_index - m_r[k].match_len;
+			int c_score = dsb_map_seed(w, m_r + k, &s_i);
+			max_score = DSB_MAX(c_score, max_score);
+		}
+		if (w->overflow)
+			return 0;
+		if (max_score > 35)
+			j -= 7;
+		if (max_score > 256) {
+			if (max_score > 512)
+				skip = 1;
+			break;
+		}
+	}
+	int top_score = 35;
+	for (uint32_t k = a_b_idx; k < w->n_anc; k++)
+		top_score = DSB_MAX(top_score, (int)w->anc[k].score);
+	for (uint32_t k = a_b_idx; k < w->n_anc; k++)
+		w->anc[k].anchor_useless = (w->anc[k].score < top_score) ? 1 : 0;
+	return skip;
+}
+
+/* fast_classify, src/cly.c:1473-1541 */
+DSB_HDN void dsb_fast_classify(dsb_read_ws *w, const dsb_sdir_t *s_d)
+{
+	dsb_spset_t sp_set = {w->spset, 0, 500};
+	uint32_t n_sv = s_d->l_seed_v_f;
+	for (uint32_t ci = 0; ci < n_sv; ci++) {
+		if (w->seeds[s_d->seed_off + ci].top == 0)
+			continue;
+		int skip = dsb_fast_seed(w, s_d, ci, &sp_set);
+		if (w->overflow)
+			return;
+		if (skip)
+			ci++;
+	}
+}
+
+/*
+ * fast_classify with one wavefront per read: the seeds of the vector are taken 64 at a time,
+ * one per lane.  Each lane runs its seed into a private staging area (anc_tmp, S anchors per
+ * lane) with its own hashed sp_set; the reference's `ci++` (skip the seed after one that
+ * scored > 512) is resolved over the group in seed order, and the kept anchors are compacted
+ * into the anchor vector in seed order (prefix sum).  A group in which some lane overflowed
+ * its staging area is replayed seed by seed in order.  hset: DSB_HSET_SLOTS x DSB_WV slots,
+ * lane-interleaved, zeroed by the caller.
+ */
+DSB_HDN void dsb_fast_classify_wave(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset)
+{
+	uint32_t lane = dsb_lane();
+	uint32_t n_sv = s_d->l_seed_v_f;
+	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV; /* dbg 32: tiny staging (tests the replay) */
+	dsb_anchor_t *stg = w->anc_tmp + (uint64_t)lane * S;
+	dsb_hset_t hs = {hset + lane, DSB_WV, 0, 0, 500};
+	int carry = 0;
+	for (uint32_t gb = 0; gb < n_sv; gb += DSB_WV) {
+		uint32_t ci = gb + lane;
+		uint32_t gn = DSB_MIN((uint32_t)DSB_WV, n_sv - gb);
+		int act = ci < n_sv && w->seeds[s_d->seed_off + ci].top != 0;
+		int trig = 0, ovf = 0;
+		uint32_t cnt = 0;
+		if (act) {
+			dsb_anchor_t *anc0 = w->anc;
+			uint32_t n0 = w->n_anc, cap0 = w->cap.anc, of0 = w->overflow;
+			w->anc = stg;
+			w->n_anc = 0;
+			w->cap.anc = S;
+			w->overflow = 0;
+			trig = dsb_fast_seed(w, s_d, ci, &hs);
+			cnt = w->n_anc;
+			ovf = w->overflow != 0;
+			w->anc = anc0;
+			w->n_anc = n0;
+			w->cap.anc = cap0;
+			w->overflow = of0;
+		}
+		/* src/cly.c:1535 `ci++`: a seed is skipped when the previous (processed) one triggered */
+		uint64_t tm = dsb_wballot(act && trig);
+		uint64_t om = dsb_wballot(act && ovf); /* an overflowed lane's trigger is not known yet */
+		uint64_t skipm = 0;
+		int carry_in = carry, prev = carry;
+		for (uint32_t k = 0; k < gn; k++) {
+			if (prev)
+				skipm |= 1ull << k;
+			prev = !prev && ((tm >> k) & 1);
+		}
+		carry = prev;
+		if ((om & ~skipm) == 0) {
+			if ((skipm >> lane) & 1)
+				cnt = 0;
+			uint32_t tot, off = dsb_wscan(cnt, &tot);
+			if (w->n_anc + tot > w->cap.anc) {
+				w->overflow |= 1;
+				dsb_wsync();
+				return;
+			}
+			for (uint32_t k = 0; k < cnt; k++)
+				w->anc[w->n_anc + off + k] = stg[k];
+			w->n_anc += tot;
+		} else { /* seed by seed, in order, deciding the skips as the reference does */
+			prev = carry_in;
+			for (uint32_t k = 0; k < gn; k++) {
+				uint32_t ck = gb + k;
+				if (prev) {
+					prev = 0;
+					continue;
+				}
+				if (w->seeds[s_d->seed_off + ck].top == 0)
+					continue;
+				if ((om >> k) & 1) { /* replay on every lane, straight into the anchor vector */
+					prev = dsb_fast_seed(w, s_d, ck, &hs);
+					if (w->overflow) {
+						dsb_wsync();
+						return;
+					}
+				} else {
+					prev = (int)((tm >> k) & 1);
+					uint32_t kc = (uint32_t)dsb_wshfl((int)cnt, (int)k);
+					if (w->n_anc + kc > w->cap.anc) {
+						w->overflow |= 1;
+						dsb_wsync();
+						return;
+					}
+					const dsb_anchor_t *src = w->anc_tmp + (uint64_t)k * S;
+					for (uint32_t e = lane; e < kc; e += DSB_WV)
+						w->anc[w->n_anc + e] = src[e];
+					w->n_anc += kc;
+				}
+				dsb_wsync();
+			}
+			carry = prev;
+		}
+		dsb_wsync();
 	}
 }
 

@@ -39,7 +39,7 @@ DSB_HD uint32_t dsb_ex_words(uint32_t L) { return (L >> 6) + 2; }
 DSB_HD uint32_t dsb_seed_cap(uint32_t L) { return (L >> 1) + 20 + L / 3 + 64; }
 
 typedef struct {
-	uint64_t bin, exF, exR, seeds, anc, anc_tmp, sidx, stmp, hit, hit_tmp, sms, hash, sch, win, mem, spset, state, total;
+	uint64_t bin, exF, exR, seeds, anc, anc_tmp, sidx, stmp, hit, hit_tmp, sms, hash, sch, win, mem, spset, hset, state, total;
 	uint32_t kl;
 } dsb_ws_layout;
 
@@ -65,6 +65,7 @@ DSB_HD dsb_ws_layout dsb_layout(uint32_t L, dsb_caps_t cap)
 	o.win = p; p = dsb_al(p + DSB_WIN_BYTES);
 	o.mem = p; p = dsb_al(p + sizeof(dsb_mem_t) * 256);
 	o.spset = p; p = dsb_al(p + 8 * 512);
+	o.hset = p; p = dsb_al(p + 8ull * DSB_HSET_SLOTS * 64); /* per-lane sp_set hashes (wave seeding) */
 	o.state = p; p = dsb_al(p + DSB_STATE_BYTES); /* dsb_rstate_t: state between phase launches */
 	o.total = p;
 	return o;

@@ -203,6 +203,49 @@ __global__ __launch_bounds__(64) void k_delA_wave(const dsb_dindex_t *__restrict
 				atomicAdd(gstats + k, (unsigned long long)st[k]);
 }
 
+/* fast_classify of one strand (phase FAST0 / FAST1) with one wavefront per read. */
+template <bool STATS>
+__global__ __launch_bounds__(64) void k_fast_wave(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+						   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+						   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+						   unsigned long long *__restrict__ gstats, int ph, uint32_t dbg)
+{
+	uint32_t t = blockIdx.x;
+	if (t >= n)
+		return;
+	uint32_t lane = threadIdx.x;
+	uint32_t r = order[t];
+	uint32_t L = len[r];
+	uint8_t *base = ws + ws_off[r];
+	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
+	dsb_ws_layout lay = dsb_layout(L, cap);
+	dsb_read_ws w;
+	dsb_ws_init(&w, ix, base, L, cap);
+	dsb_rstate_t *sp = (dsb_rstate_t *)(base + lay.state);
+	dsb_rflags_t f;
+	dsb_state_load(&w, &f, sp);
+	if (!dsb_phase_active(&w, &f, ph))
+		return;
+	w.dbg = dbg;
+	uint64_t st[DSB_ST_N];
+	if (STATS) {
+		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
+		w.stats = st;
+	}
+	uint64_t *hset = (uint64_t *)(base + lay.hset);
+	for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
+		hset[k] = 0;
+	__syncthreads();
+	dsb_fast_classify_wave(&w, &w.sd[ph - DSB_PH_FAST0], hset);
+	__syncthreads();
+	if (lane == 0)
+		dsb_state_save(&w, &f, sp);
+	if (STATS)
+		for (int k = 0; k < DSB_ST_N; k++)
+			if (st[k])
+				atomicAdd(gstats + k, (unsigned long long)st[k]);
+}
+
 template <bool STATS>
 __global__ __launch_bounds__(64) void k_classB(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 						const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
@@ -514,7 +557,11 @@ static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl,
 			 uint32_t m)
 {
 	hipStream_t s = g->stream;
-	if (ph == DSB_PH_DELA)
+	if ((ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) && !(wave_dbg() & 16))
+		hipLaunchKernelGGL(stats ? k_fast_wave<true> : k_fast_wave<false>, dim3(m), dim3(64), 0, s, g->d, cl,
+				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m,
+				   g->stats.as<unsigned long long>(), ph, wave_dbg());
+	else if (ph == DSB_PH_DELA)
 		hipLaunchKernelGGL(stats ? k_delA_wave<true> : k_delA_wave<false>, dim3(m), dim3(64), 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
 				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), wave_dbg());

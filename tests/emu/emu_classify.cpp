@@ -74,6 +74,7 @@ int main(int argc, char **argv)
 			dsb_read_ws w;
 			dsb_ws_init(&w, &d, arena.data(), L, cap);
 			if (stats) w.stats = st;
+			if (getenv("EMU_DBG")) w.dbg = (uint32_t)strtoul(getenv("EMU_DBG"), 0, 0);
 			/* encode (CLY_Bit) + reverse complement + guards (src/cly.c:1245-1254) */
 			for (uint32_t k = 0; k < L; k++) w.bin[k] = dsb_cly_bit(seq[k]);
 			for (uint32_t k = 0; k < L; k++) w.bin[L + L - 1 - k] = 3 - w.bin[k];
@@ -92,7 +93,14 @@ int main(int argc, char **argv)
 			}
 			if (getenv("EMU_WAVE")) { /* the wave-cooperative code paths, as a one-lane wave */
 				dsb_rflags_t f = {0, 0, 0, 0};
-				for (int ph = 0; ph < DSB_PH_DELA; ph++) dsb_phase(&w, &f, ph);
+				uint64_t *hset = (uint64_t *)(arena.data() + lay.hset);
+				for (int ph = 0; ph < DSB_PH_DELA; ph++) {
+					if ((ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) && dsb_phase_active(&w, &f, ph)) {
+						memset(hset, 0, 8ull * DSB_HSET_SLOTS * 64);
+						dsb_fast_classify_wave(&w, &w.sd[ph - DSB_PH_FAST0], hset);
+					} else
+						dsb_phase(&w, &f, ph);
+				}
 				if (dsb_phase_active(&w, &f, DSB_PH_DELA)) dsb_delete_small_A<true>(&w);
 			} else
 				dsb_classify_A(&w);
