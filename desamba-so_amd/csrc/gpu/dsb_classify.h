@@ -947,17 +947,68 @@ DSB_HD void dsb_chain_insert_M2(dsb_read_ws *w, uint32_t ai)
 }
 
 /* chain_insert_M3, src/cly.c:237-322 (anchors sorted in place first, src/cly.c:242) */
-DSB_HDN void dsb_chain_insert_M3(dsb_read_ws *w)
+/* Anchor_cmp_by_chr_ID_and_pos under glibc msort == stable ascending sort by
+ * (ref_ID, direction, ref_offset).  WAVE: bitonic sort of (key, index) pairs (a total order,
+ * so the same permutation as any stable sort), keys/indices staged in hit_tmp. */
+template <bool WAVE>
+DSB_HD void dsb_sort_anchors(dsb_read_ws *w)
 {
 	uint32_t n = w->n_anc;
 	dsb_anchor_t *A = w->anc;
-	{
+	if (!WAVE || (w->dbg & 64)) {
 		uint32_t *idx = w->sidx, *tmp = w->stmp;
 		for (uint32_t k = 0; k < n; k++) idx[k] = k;
 		dsb_msort(idx, tmp, n, [A](uint32_t ia, uint32_t ib) -> int { return dsb_anchor_cmp(A + ia, A + ib); });
 		for (uint32_t k = 0; k < n; k++) w->anc_tmp[k] = A[idx[k]];
 		for (uint32_t k = 0; k < n; k++) A[k] = w->anc_tmp[k];
+		return;
 	}
+	uint32_t lane = dsb_lane();
+	uint32_t N = 1;
+	while (N < n) N <<= 1;
+	uint64_t *key = (uint64_t *)w->hit_tmp;
+	uint32_t *id = (uint32_t *)(key + N);
+	for (uint32_t k = lane; k < N; k += DSB_WV) {
+		if (k < n) {
+			key[k] = ((uint64_t)A[k].ref_ID << 33) | ((uint64_t)(A[k].direction != 0) << 32) | A[k].ref_offset;
+			id[k] = k;
+		} else {
+			key[k] = ~0ull;
+			id[k] = 0xffffffffu;
+		}
+	}
+	dsb_wsync();
+	for (uint32_t size = 2; size <= N; size <<= 1) {
+		for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+			for (uint32_t t = lane; t < N / 2; t += DSB_WV) {
+				uint32_t lo = ((t / stride) * stride << 1) + (t % stride);
+				uint32_t hi = lo + stride;
+				int asc = ((lo & size) == 0);
+				uint64_t ka = key[lo], kb = key[hi];
+				uint32_t ia = id[lo], ib = id[hi];
+				int gt = (ka > kb) || (ka == kb && ia > ib);
+				if (gt == asc) {
+					key[lo] = kb; key[hi] = ka;
+					id[lo] = ib; id[hi] = ia;
+				}
+			}
+			dsb_wsync();
+		}
+	}
+	for (uint32_t k = lane; k < n; k += DSB_WV)
+		w->anc_tmp[k] = A[id[k]];
+	dsb_wsync();
+	for (uint32_t k = lane; k < n; k += DSB_WV)
+		A[k] = w->anc_tmp[k];
+	dsb_wsync();
+}
+
+template <bool WAVE>
+DSB_HDN void dsb_chain_insert_M3(dsb_read_ws *w)
+{
+	uint32_t n = w->n_anc;
+	dsb_anchor_t *A = w->anc;
+	dsb_sort_anchors<WAVE>(w);
 	int *score_v = (int *)w->stmp; /* 1024 ints; stmp is free again */
 	for (uint32_t chr_st = 0; chr_st < n;) {
 		uint32_t chr_ed = chr_st + 1;
@@ -976,20 +1027,62 @@ DSB_HDN void dsb_chain_insert_M3(dsb_read_ws *w)
 			anchor_max_score = c_a->score;
 			uint32_t max_t = c_a->ref_offset + 3;
 			uint32_t max_q = c_a->index_in_read + 3;
-			for (int64_t pi = (int64_t)ca - 1; pi >= (int64_t)chr_st; pi--) {
-				dsb_anchor_t *pre = A + pi;
-				if (pre->index_in_read + pre->mtch_len > max_q) continue;
-				if (pre->ref_offset + pre->mtch_len > max_t) continue;
-				if (pre->index_in_read + 1000 < max_q) break;
-				if (pre->ref_offset + 1000 < max_t) break;
-				int indel = (int)(pre->index_in_read - pre->ref_offset - (max_q - max_t));
-				int ABS_indel = DSB_ABS(indel);
-				if (ABS_indel > 200) continue;
-				int new_score = (int)((uint32_t)(score_v[pi - chr_st] + c_a->mtch_len - (ABS_indel >> 4)) -
-						      ((max_q - pre->index_in_read) >> 8));
-				if (new_score > anchor_max_score) {
-					anchor_max_score = new_score;
-					c_a->pre = (int32_t)pi;
+			if (!WAVE || (w->dbg & 64)) {
+				for (int64_t pi = (int64_t)ca - 1; pi >= (int64_t)chr_st; pi--) {
+					dsb_anchor_t *pre = A + pi;
+					if (pre->index_in_read + pre->mtch_len > max_q) continue;
+					if (pre->ref_offset + pre->mtch_len > max_t) continue;
+					if (pre->index_in_read + 1000 < max_q) break;
+					if (pre->ref_offset + 1000 < max_t) break;
+					int indel = (int)(pre->index_in_read - pre->ref_offset - (max_q - max_t));
+					int ABS_indel = DSB_ABS(indel);
+					if (ABS_indel > 200) continue;
+					int new_score = (int)((uint32_t)(score_v[pi - chr_st] + c_a->mtch_len - (ABS_indel >> 4)) -
+							      ((max_q - pre->index_in_read) >> 8));
+					if (new_score > anchor_max_score) {
+						anchor_max_score = new_score;
+						c_a->pre = (int32_t)pi;
+					}
+				}
+			} else { /* best (score, highest index) over the scan, stopped at the first break */
+				uint32_t lane = dsb_lane();
+				uint64_t best = 0;
+				for (int64_t pb = (int64_t)ca - 1; pb >= (int64_t)chr_st; pb -= DSB_WV) {
+					int64_t pi = pb - (int64_t)lane;
+					uint64_t cand = 0;
+					int brk = 0;
+					if (pi >= (int64_t)chr_st) {
+						dsb_anchor_t *pre = A + pi;
+						if (!(pre->index_in_read + pre->mtch_len > max_q) && !(pre->ref_offset + pre->mtch_len > max_t)) {
+							if (pre->index_in_read + 1000 < max_q || pre->ref_offset + 1000 < max_t)
+								brk = 1;
+							else {
+								int indel = (int)(pre->index_in_read - pre->ref_offset - (max_q - max_t));
+								int ABS_indel = DSB_ABS(indel);
+								if (ABS_indel <= 200) {
+									int new_score = (int)((uint32_t)(score_v[pi - chr_st] + c_a->mtch_len -
+												 (ABS_indel >> 4)) -
+											      ((max_q - pre->index_in_read) >> 8));
+									cand = ((uint64_t)((uint32_t)new_score ^ 0x80000000u) << 32) |
+									       (uint32_t)(pi + 1);
+								}
+							}
+						}
+					}
+					uint64_t bm = dsb_wballot(brk);
+					if (bm && lane >= (uint32_t)__builtin_ctzll(bm))
+						cand = 0;
+					best = DSB_MAX(best, cand);
+					if (bm)
+						break;
+				}
+				best = dsb_wmax64(best);
+				if (best) {
+					int bs = (int)((uint32_t)(best >> 32) ^ 0x80000000u);
+					if (bs > anchor_max_score) {
+						anchor_max_score = bs;
+						c_a->pre = (int32_t)((uint32_t)best - 1);
+					}
 				}
 			}
 			score_v[ca - chr_st] = anchor_max_score;
@@ -1063,6 +1156,7 @@ DSB_HD void dsb_sort_chains(dsb_read_ws *w, Cmp cmp)
 }
 
 /* resolve_tree, src/cly.c:325-348 */
+template <bool WAVE>
 DSB_HDN void dsb_resolve_tree(dsb_read_ws *w)
 {
 	w->n_hit = 0;
@@ -1070,7 +1164,7 @@ DSB_HDN void dsb_resolve_tree(dsb_read_ws *w)
 		for (uint32_t k = 0; k < w->n_anc; k++)
 			dsb_chain_insert_M2(w, k);
 	else
-		dsb_chain_insert_M3(w);
+		dsb_chain_insert_M3<WAVE>(w);
 	if (w->overflow)
 		return;
 	if (w->n_hit > 1)
@@ -2094,6 +2188,7 @@ DSB_HD int dsb_phase_active(const dsb_read_ws *w, const dsb_rflags_t *f, int ph)
 	}
 }
 
+template <bool WAVE = false>
 DSB_HD void dsb_phase(dsb_read_ws *w, dsb_rflags_t *f, int ph)
 {
 	if (!dsb_phase_active(w, f, ph))
@@ -2120,7 +2215,7 @@ DSB_HD void dsb_phase(dsb_read_ws *w, dsb_rflags_t *f, int ph)
 		dsb_fast_classify(w, &w->sd[1]);
 		return;
 	case DSB_PH_RESOLVE_F:
-		dsb_resolve_tree(w);
+		dsb_resolve_tree<WAVE>(w);
 		if (w->overflow)
 			return;
 		if (w->n_hit <= 0)
@@ -2137,7 +2232,7 @@ DSB_HD void dsb_phase(dsb_read_ws *w, dsb_rflags_t *f, int ph)
 		dsb_slow_classify(w, &w->sd[0]);
 		return;
 	case DSB_PH_RESOLVE_S0:
-		dsb_resolve_tree(w);
+		dsb_resolve_tree<WAVE>(w);
 		if (w->overflow)
 			return;
 		f->slow1 = (f->both || w->n_hit <= 0 || (w->hit[0].anchor_number < 5 && super_repeat < 3));
@@ -2146,10 +2241,10 @@ DSB_HD void dsb_phase(dsb_read_ws *w, dsb_rflags_t *f, int ph)
 		dsb_slow_classify(w, &w->sd[1]);
 		return;
 	case DSB_PH_RESOLVE_S1:
-		dsb_resolve_tree(w);
+		dsb_resolve_tree<WAVE>(w);
 		return;
 	case DSB_PH_DELA:
-		dsb_delete_small_A<false>(w);
+		dsb_delete_small_A<WAVE>(w);
 		return;
 	}
 }

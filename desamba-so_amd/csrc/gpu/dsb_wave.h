@@ -37,6 +37,15 @@ DSB_HD uint32_t dsb_wscan(uint32_t v, uint32_t *tot)
 	*tot = __shfl(x, 63);
 	return x - v;
 }
+DSB_HD uint64_t dsb_wmax64(uint64_t v)
+{
+	for (int o = 32; o; o >>= 1) {
+		uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
+		uint64_t u = ((uint64_t)hi << 32) | lo;
+		v = u > v ? u : v;
+	}
+	return v;
+}
 DSB_HD uint64_t dsb_wballot(int p) { return __ballot(p); }
 DSB_HD int dsb_wshfl(int v, int src) { return __shfl(v, src); }
 #else
@@ -45,6 +54,7 @@ DSB_HD uint32_t dsb_lane(void) { return 0; }
 DSB_HD void dsb_wsync(void) {}
 DSB_HD int dsb_wmax(int v) { return v; }
 DSB_HD uint32_t dsb_wscan(uint32_t v, uint32_t *tot) { *tot = v; return 0; }
+DSB_HD uint64_t dsb_wmax64(uint64_t v) { return v; }
 DSB_HD uint64_t dsb_wballot(int p) { return p ? 1 : 0; }
 DSB_HD int dsb_wshfl(int v, int src) { (void)src; return v; }
 #endif

@@ -152,63 +152,15 @@ __global__ __launch_bounds__(64) void k_phase(const dsb_dindex_t *__restrict__ i
 			atomicAdd(gstats + k, (unsigned long long)st[k]);
 }
 
-/* The last phase of part A (delete_small_score_rst A: read hash, sparse-DP scoring of every
- * chain, merge) with one wavefront per read (dsb_wave.h); one wave per workgroup. */
+/* One phase of part A with one wavefront per read (dsb_wave.h), one wave per workgroup:
+ * fast seeding (FAST0/FAST1), chaining (RESOLVE_*), scoring (DELA).  The last phase
+ * publishes the read's summary like k_phase. */
 template <bool STATS>
-__global__ __launch_bounds__(64) void k_delA_wave(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
-						   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
-						   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
-						   dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
-						   unsigned long long *__restrict__ gstats, uint32_t dbg)
-{
-	uint32_t t = blockIdx.x;
-	if (t >= n)
-		return;
-	uint32_t lane = threadIdx.x;
-	uint32_t r = order[t];
-	uint32_t L = len[r];
-	uint8_t *base = ws + ws_off[r];
-	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
-	dsb_read_ws w;
-	dsb_ws_init(&w, ix, base, L, cap);
-	dsb_rstate_t *sp = (dsb_rstate_t *)(base + dsb_layout(L, cap).state);
-	dsb_rflags_t f;
-	dsb_state_load(&w, &f, sp);
-	w.dbg = dbg;
-	uint64_t st[DSB_ST_N];
-	if (STATS) {
-		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
-		w.stats = st;
-	}
-	if (dsb_phase_active(&w, &f, DSB_PH_DELA))
-		dsb_delete_small_A<true>(&w);
-	__syncthreads();
-	if (lane == 0) {
-		dsb_state_save(&w, &f, sp);
-		dsb_read_out_t o;
-		o.n_hit = w.n_hit;
-		o.n_anchor = w.n_anc;
-		o.fast = w.fast_classify;
-		o.status = w.overflow;
-		o.reached_update = w.reached_update;
-		o.pad = 0;
-		o.hit_off = 0;
-		ro[r] = o;
-		if (w.overflow)
-			atomicAdd(n_overflow, 1u);
-	}
-	if (STATS)
-		for (int k = 0; k < DSB_ST_N; k++)
-			if (st[k])
-				atomicAdd(gstats + k, (unsigned long long)st[k]);
-}
-
-/* fast_classify of one strand (phase FAST0 / FAST1) with one wavefront per read. */
-template <bool STATS>
-__global__ __launch_bounds__(64) void k_fast_wave(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
-						   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
-						   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
-						   unsigned long long *__restrict__ gstats, int ph, uint32_t dbg)
+__global__ __launch_bounds__(64) void k_wave_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+						    const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+						    uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+						    dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
+						    unsigned long long *__restrict__ gstats, int ph, uint32_t dbg)
 {
 	uint32_t t = blockIdx.x;
 	if (t >= n)
@@ -224,22 +176,41 @@ __global__ __launch_bounds__(64) void k_fast_wave(const dsb_dindex_t *__restrict
 	dsb_rstate_t *sp = (dsb_rstate_t *)(base + lay.state);
 	dsb_rflags_t f;
 	dsb_state_load(&w, &f, sp);
-	if (!dsb_phase_active(&w, &f, ph))
-		return;
 	w.dbg = dbg;
 	uint64_t st[DSB_ST_N];
 	if (STATS) {
 		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
 		w.stats = st;
 	}
-	uint64_t *hset = (uint64_t *)(base + lay.hset);
-	for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
-		hset[k] = 0;
+	int active = dsb_phase_active(&w, &f, ph);
+	if (active) {
+		if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
+			uint64_t *hset = (uint64_t *)(base + lay.hset);
+			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
+				hset[k] = 0;
+			__syncthreads();
+			dsb_fast_classify_wave(&w, &w.sd[ph - DSB_PH_FAST0], hset);
+		} else
+			dsb_phase<true>(&w, &f, ph);
+	}
 	__syncthreads();
-	dsb_fast_classify_wave(&w, &w.sd[ph - DSB_PH_FAST0], hset);
-	__syncthreads();
-	if (lane == 0)
-		dsb_state_save(&w, &f, sp);
+	if (lane == 0) {
+		if (active)
+			dsb_state_save(&w, &f, sp);
+		if (ph == DSB_PH_DELA) {
+			dsb_read_out_t o;
+			o.n_hit = w.n_hit;
+			o.n_anchor = w.n_anc;
+			o.fast = w.fast_classify;
+			o.status = w.overflow;
+			o.reached_update = w.reached_update;
+			o.pad = 0;
+			o.hit_off = 0;
+			ro[r] = o;
+			if (w.overflow)
+				atomicAdd(n_overflow, 1u);
+		}
+	}
 	if (STATS)
 		for (int k = 0; k < DSB_ST_N; k++)
 			if (st[k])
@@ -512,7 +483,9 @@ static float ev_ms(dsb_gpu_dev *g)
 	return ms;
 }
 
-static size_t ws_budget(void)
+/* workspace budget for one chunk of reads: most of the HBM left after the index (the
+ * workspace already held by this device counts as available) */
+static size_t ws_budget(const dsb_gpu_dev *g)
 {
 	const char *e = getenv("DSB_WS_BUDGET_MB");
 	if (e)
@@ -520,8 +493,8 @@ static size_t ws_budget(void)
 	size_t fr = 0, tot = 0;
 	if (hipMemGetInfo(&fr, &tot) != hipSuccess)
 		return (size_t)8 << 30;
-	size_t b = fr / 2;
-	size_t cap = (size_t)48 << 30;
+	size_t b = (size_t)((double)(fr + g->ws.cap) * 0.6); /* + 1/4 reserved for overflow re-runs */
+	size_t cap = (size_t)200 << 30;
 	return b < cap ? b : cap;
 }
 
@@ -551,20 +524,25 @@ static uint32_t wave_dbg(void)
 	return e ? (uint32_t)strtoul(e, NULL, 0) : 0;
 }
 
-/* one phase of part A over the reads order[0..m): lane-per-read kernels, except the
- * scoring phase (one wavefront per read) */
+/* phases run with one wavefront per read (DSB_WAVE_PHASES overrides, for diagnostics) */
+static uint32_t wave_phases(void)
+{
+	const char *e = getenv("DSB_WAVE_PHASES");
+	if (e)
+		return (uint32_t)strtoul(e, NULL, 0);
+	return (1u << DSB_PH_FAST0) | (1u << DSB_PH_FAST1) | (1u << DSB_PH_RESOLVE_F) | (1u << DSB_PH_RESOLVE_S0) |
+	       (1u << DSB_PH_RESOLVE_S1) | (1u << DSB_PH_DELA);
+}
+
+/* one phase of part A over the reads order[0..m) */
 static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl, uint8_t *wsb, const uint32_t *order,
 			 uint32_t m)
 {
 	hipStream_t s = g->stream;
-	if ((ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) && !(wave_dbg() & 16))
-		hipLaunchKernelGGL(stats ? k_fast_wave<true> : k_fast_wave<false>, dim3(m), dim3(64), 0, s, g->d, cl,
-				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m,
-				   g->stats.as<unsigned long long>(), ph, wave_dbg());
-	else if (ph == DSB_PH_DELA)
-		hipLaunchKernelGGL(stats ? k_delA_wave<true> : k_delA_wave<false>, dim3(m), dim3(64), 0, s, g->d, cl,
+	if ((wave_phases() >> ph) & 1)
+		hipLaunchKernelGGL(stats ? k_wave_phase<true> : k_wave_phase<false>, dim3(m), dim3(64), 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
-				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), wave_dbg());
+				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), ph, wave_dbg());
 	else
 		hipLaunchKernelGGL(phase_kernel_at(ph, stats), dim3((m + 63) / 64), dim3(64), 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
@@ -640,7 +618,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	std::vector<uint64_t> word_off;
 	dsb_read_out_t *ro = b->ro.data();
 	std::vector<dsb_hit_out_t> &hv = b->hits;
-	size_t budget = ws_budget();
+	size_t budget = ws_budget(g);
 	int carry = *max_read_l;
 	int l_ek = ix->l_ek;
 	for (uint64_t cb = 0; cb < n;) {
@@ -656,7 +634,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		}
 		uint32_t cn = (uint32_t)(ce - cb);
 		T.n_chunks++;
-		if (g->ws.ensure(ws_total + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
+		if (g->ws.ensure(ws_total + ws_total / 4 + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
 		    g->word_off.ensure(8 * (size_t)cn + 16, err, errn))
 			return -1;
 		HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
@@ -711,7 +689,9 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				ws_off[cb + i] = ws_total + tot2;
 				tot2 += dsb_layout(len[cb + i], dsb_default_caps(len[cb + i], scale[cb + i])).total;
 			}
-			{ /* grow the chunk workspace, keeping the first ws_total bytes */
+			if (ws_total + tot2 + 4096 <= g->ws.cap) { /* fits the reserve */
+				ws_total += tot2;
+			} else { /* grow the chunk workspace, keeping the first ws_total bytes */
 				void *np = nullptr;
 				size_t need = ws_total + tot2 + 4096;
 				HIP_OK(hipMalloc(&np, need));

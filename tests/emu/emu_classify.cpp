@@ -99,9 +99,9 @@ int main(int argc, char **argv)
 						memset(hset, 0, 8ull * DSB_HSET_SLOTS * 64);
 						dsb_fast_classify_wave(&w, &w.sd[ph - DSB_PH_FAST0], hset);
 					} else
-						dsb_phase(&w, &f, ph);
+						dsb_phase<true>(&w, &f, ph);
 				}
-				if (dsb_phase_active(&w, &f, DSB_PH_DELA)) dsb_delete_small_A<true>(&w);
+				dsb_phase<true>(&w, &f, DSB_PH_DELA);
 			} else
 				dsb_classify_A(&w);
 			if (getenv("DSB_DEBUG_READ") && strtoull(getenv("DSB_DEBUG_READ"), 0, 10) == i)
