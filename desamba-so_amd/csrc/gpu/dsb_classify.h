@@ -92,7 +92,7 @@ typedef struct {
 	uint32_t *hh[2], *ht[2], *hn[2], *hk[2]; /* read 9-mer hash: heads, tails, next, kmer */
 	dsb_sch_t *sch;         /* 256 + 2*400 */
 	uint8_t *win;           /* DSB_WIN_BYTES: sdp_middle ref[2000] and sdp_right/left ref[1000] windows */
-	dsb_mem_t *mem;         /* 256 MEM results (slow mode) */
+	dsb_mem_t *mem;         /* 16 MEM results per lane (slow mode) */
 	uint64_t *spset;        /* 500 */
 	dsb_caps_t cap;
 	uint32_t overflow;
@@ -813,61 +813,146 @@ DSB_HDN void dsb_fast_classify_wave(dsb_read_ws *w, const dsb_sdir_t *s_d, uint6
 
 #define DSB_MEM_SEARCH_SLOW 8
 #define DSB_MIN_MEM_LEN_SLOW 20
-/* slow_classify, src/cly.c:1545-1606 */
-DSB_HDN void dsb_slow_classify(dsb_read_ws *w, const dsb_sdir_t *sd)
+/* One seed of slow_classify (src/cly.c:1556-1603): MEM searches every other position of the
+ * seed, the hits ordered by match length (stable msort, MEM_rst_cmp_by_match_len) and the
+ * first 8 mapped.  Only those 8 are ever used, so they are kept as a stable top-8 while the
+ * hits stream in (tmp: 16 entries).  The seed's anchors below its top score become useless. */
+template <typename SET>
+DSB_HD void dsb_slow_seed(dsb_read_ws *w, const dsb_sdir_t *sd, uint32_t i, SET *sp_set, dsb_mem_t *tmp)
 {
 	const dsb_dindex_t *ix = w->ix;
 	int l_ek = ix->l_ek;
 	uint8_t *bin_read = w->bin + (sd->strand ? w->L : 0);
-	dsb_seed_t *sv_f = w->seeds + sd->seed_off;
+	dsb_seed_t *sv = w->seeds + sd->seed_off + i;
+	int min_match_len = DSB_MIN(DSB_MIN_MEM_LEN_SLOW - 1, l_ek + 1);
+	dsb_set_reset(sp_set);
+	dsb_mem_t *top = tmp, *cur = tmp + DSB_MEM_SEARCH_SLOW;
+	int n_top = 0, total = 0;
+	for (int j = (int)sv->len - 1; j >= 1; j -= 2) {
+		int k_idx = (int)sv->offset + j;
+		uint64_t kmer = dsb_kmer_at(bin_read + k_idx, l_ek, ix->single_base_max);
+		uint64_t pre_v = kmer & DSB_PRE_IDX_MASK;
+		int s_idx = k_idx + l_ek - 1;
+		int c = dsb_mem_search(w, bin_read + s_idx, pre_v, DSB_MEM_SEARCH_SLOW, min_match_len, s_idx, sp_set, cur);
+		for (int k = 0; k < c; k++) {
+			cur[k].read_offset = k_idx + l_ek - 1 - cur[k].match_len;
+			int p = 0; /* stable, match_len descending: after every kept hit at least as long */
+			while (p < n_top && top[p].match_len >= cur[k].match_len)
+				p++;
+			if (p >= DSB_MEM_SEARCH_SLOW)
+				continue;
+			for (int q = DSB_MIN(n_top, DSB_MEM_SEARCH_SLOW - 1); q > p; q--)
+				top[q] = top[q - 1];
+			top[p] = cur[k];
+			n_top = DSB_MIN(n_top + 1, DSB_MEM_SEARCH_SLOW);
+		}
+		total += c;
+	}
+	if (total == 0)
+		return;
+	dsb_seedinfo_t seed_info = {bin_read, w->L, (uint16_t)i, sd->direction};
+	uint32_t a_b_idx = w->n_anc;
+	for (int k = 0; k < n_top; k++)
+		dsb_map_seed(w, top + k, &seed_info);
+	if (w->overflow)
+		return;
+	int top_score = 35;
+	for (uint32_t k = a_b_idx; k < w->n_anc; k++)
+		top_score = DSB_MAX(top_score, (int)w->anc[k].score);
+	for (uint32_t k = a_b_idx; k < w->n_anc; k++)
+		w->anc[k].anchor_useless = (w->anc[k].score < top_score) ? 1 : 0;
+}
+
+/* src/cly.c:1563: the guard reads seed 0's `top`, not seed i's (H10) */
+DSB_HD int dsb_slow_takes(const dsb_read_ws *w, const dsb_sdir_t *sd, uint32_t i)
+{
+	const dsb_seed_t *sv_f = w->seeds + sd->seed_off;
+	return !((int)(sv_f[i].len) < 3 && sv_f->top == 0);
+}
+
+/* slow_classify, src/cly.c:1545-1606 */
+DSB_HDN void dsb_slow_classify(dsb_read_ws *w, const dsb_sdir_t *sd)
+{
 	dsb_spset_t sp_set = {w->spset, 0, 500};
-	dsb_mem_t *mem_rst = w->mem;
-	dsb_seedinfo_t seed_info = {bin_read, w->L, 0, sd->direction};
 	for (uint32_t i = 0; i < sd->l_seed_v_f; i++) {
-		if ((int)(sv_f[i].len) < 3 && sv_f->top == 0) /* checks seed 0's top (H10) */
+		if (!dsb_slow_takes(w, sd, i))
 			continue;
-		int min_match_len = DSB_MIN(DSB_MIN_MEM_LEN_SLOW - 1, l_ek + 1);
-		sp_set.l = 0;
-		int mem_rst_num = 0;
-		for (int j = (int)sv_f[i].len - 1; j >= 1; j -= 2) {
-			int k_idx = (int)sv_f[i].offset + j;
-			uint64_t kmer = dsb_kmer_at(bin_read + k_idx, l_ek, ix->single_base_max);
-			uint64_t pre_v = kmer & DSB_PRE_IDX_MASK;
-			int s_idx = k_idx + l_ek - 1;
-			if (mem_rst_num + DSB_MEM_SEARCH_SLOW > 256) { /* cannot happen: seeds <= 61 long */
-				w->overflow |= 2;
-				return;
-			}
-			int c = dsb_mem_search(w, bin_read + s_idx, pre_v, DSB_MEM_SEARCH_SLOW, min_match_len, s_idx,
-					       &sp_set, mem_rst + mem_rst_num);
-			for (int k = mem_rst_num; k < mem_rst_num + c; k++)
-				mem_rst[k].read_offset = k_idx + l_ek - 1 - mem_rst[k].match_len;
-			mem_rst_num += c;
-		}
-		if (mem_rst_num == 0)
-			continue;
-		if (mem_rst_num > 1) {
-			/* qsort by match_len descending (MEM_rst_cmp_by_match_len, :1325-1328): stable */
-			uint32_t *idx = w->sidx, *tmp = w->stmp;
-			for (int k = 0; k < mem_rst_num; k++) idx[k] = k;
-			dsb_mem_t *mr = mem_rst;
-			dsb_msort(idx, tmp, (uint32_t)mem_rst_num, [mr](uint32_t a, uint32_t b) -> int { return dsb_mem_cmp(mr + a, mr + b); });
-			dsb_mem_t *scratch = (dsb_mem_t *)w->anc_tmp; /* free while not chaining */
-			for (int k = 0; k < mem_rst_num; k++) scratch[k] = mem_rst[idx[k]];
-			for (int k = 0; k < mem_rst_num; k++) mem_rst[k] = scratch[k];
-		}
-		seed_info.seed_ID = (uint16_t)i;
-		uint32_t a_b_idx = w->n_anc;
-		int max_search = DSB_MIN(mem_rst_num, DSB_MEM_SEARCH_SLOW);
-		for (int k = 0; k < max_search; k++)
-			dsb_map_seed(w, mem_rst + k, &seed_info);
+		dsb_slow_seed(w, sd, i, &sp_set, w->mem);
 		if (w->overflow)
 			return;
-		int top_score = 35;
-		for (uint32_t k = a_b_idx; k < w->n_anc; k++)
-			top_score = DSB_MAX(top_score, (int)w->anc[k].score);
-		for (uint32_t k = a_b_idx; k < w->n_anc; k++)
-			w->anc[k].anchor_useless = (w->anc[k].score < top_score) ? 1 : 0;
+	}
+	w->fast_classify = 0;
+}
+
+/* slow_classify with one wavefront per read, seeds across lanes (as dsb_fast_classify_wave,
+ * without the skip rule).  memtmp: 16 MEM results per lane. */
+DSB_HDN void dsb_slow_classify_wave(dsb_read_ws *w, const dsb_sdir_t *sd, uint64_t *hset, dsb_mem_t *memtmp)
+{
+	uint32_t lane = dsb_lane();
+	uint32_t n_sv = sd->l_seed_v_f;
+	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV;
+	dsb_anchor_t *stg = w->anc_tmp + (uint64_t)lane * S;
+	dsb_hset_t hs = {hset + lane, DSB_WV, 0, 0, 500};
+	dsb_mem_t *mt = memtmp + (uint64_t)lane * (2 * DSB_MEM_SEARCH_SLOW);
+	for (uint32_t gb = 0; gb < n_sv; gb += DSB_WV) {
+		uint32_t ci = gb + lane;
+		uint32_t gn = DSB_MIN((uint32_t)DSB_WV, n_sv - gb);
+		int act = ci < n_sv && dsb_slow_takes(w, sd, ci);
+		int ovf = 0;
+		uint32_t cnt = 0;
+		if (act) {
+			dsb_anchor_t *anc0 = w->anc;
+			uint32_t n0 = w->n_anc, cap0 = w->cap.anc, of0 = w->overflow;
+			w->anc = stg;
+			w->n_anc = 0;
+			w->cap.anc = S;
+			w->overflow = 0;
+			dsb_slow_seed(w, sd, ci, &hs, mt);
+			cnt = w->n_anc;
+			ovf = w->overflow != 0;
+			w->anc = anc0;
+			w->n_anc = n0;
+			w->cap.anc = cap0;
+			w->overflow = of0;
+		}
+		uint64_t om = dsb_wballot(act && ovf);
+		if (om == 0) {
+			uint32_t tot, off = dsb_wscan(cnt, &tot);
+			if (w->n_anc + tot > w->cap.anc) {
+				w->overflow |= 1;
+				dsb_wsync();
+				return;
+			}
+			for (uint32_t k = 0; k < cnt; k++)
+				w->anc[w->n_anc + off + k] = stg[k];
+			w->n_anc += tot;
+		} else {
+			for (uint32_t k = 0; k < gn; k++) {
+				uint32_t ck = gb + k;
+				if (!dsb_slow_takes(w, sd, ck))
+					continue;
+				if ((om >> k) & 1) {
+					dsb_slow_seed(w, sd, ck, &hs, mt);
+					if (w->overflow) {
+						dsb_wsync();
+						return;
+					}
+				} else {
+					uint32_t kc = (uint32_t)dsb_wshfl((int)cnt, (int)k);
+					if (w->n_anc + kc > w->cap.anc) {
+						w->overflow |= 1;
+						dsb_wsync();
+						return;
+					}
+					const dsb_anchor_t *src = w->anc_tmp + (uint64_t)k * S;
+					for (uint32_t e = lane; e < kc; e += DSB_WV)
+						w->anc[w->n_anc + e] = src[e];
+					w->n_anc += kc;
+				}
+				dsb_wsync();
+			}
+		}
+		dsb_wsync();
 	}
 	w->fast_classify = 0;
 }

@@ -63,7 +63,7 @@ DSB_HD dsb_ws_layout dsb_layout(uint32_t L, dsb_caps_t cap)
 	o.hash = p; p = dsb_al(p + 2ull * (8ull * (1ull << o.kl) + 8ull * L));
 	o.sch = p; p = dsb_al(p + sizeof(dsb_sch_t) * (256 + 2 * 400 + 64));
 	o.win = p; p = dsb_al(p + DSB_WIN_BYTES);
-	o.mem = p; p = dsb_al(p + sizeof(dsb_mem_t) * 256);
+	o.mem = p; p = dsb_al(p + sizeof(dsb_mem_t) * 16 * 64); /* 16 MEM results per lane (slow seeding) */
 	o.spset = p; p = dsb_al(p + 8 * 512);
 	o.hset = p; p = dsb_al(p + 8ull * DSB_HSET_SLOTS * 64); /* per-lane sp_set hashes (wave seeding) */
 	o.state = p; p = dsb_al(p + DSB_STATE_BYTES); /* dsb_rstate_t: state between phase launches */

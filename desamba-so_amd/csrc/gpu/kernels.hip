@@ -25,6 +25,25 @@
 #include <algorithm>
 #include "dsb_ws.h"
 #include "dsb_gpu.h"
+
+/* minimum waves per SIMD requested from the register allocator (spills beyond) */
+/* measured on MI355X (C1 workload): fast seeding is fastest at 2 waves/SIMD, the scoring
+ * phase at 4, the lane-per-read phases at 2 (profiles/) */
+#ifndef DSB_MINW_LANE
+#define DSB_MINW_LANE 2
+#endif
+#ifndef DSB_MINW_FAST
+#define DSB_MINW_FAST 2
+#endif
+#ifndef DSB_MINW_DELA
+#define DSB_MINW_DELA 4
+#endif
+#ifndef DSB_MINW_RESOLVE
+#define DSB_MINW_RESOLVE 4
+#endif
+#define DSB_MINW_WAVE(PH) ((PH) == DSB_PH_DELA ? DSB_MINW_DELA : \
+			   ((PH) == DSB_PH_FAST0 || (PH) == DSB_PH_FAST1 || (PH) == DSB_PH_SLOW0 || (PH) == DSB_PH_SLOW1) \
+			   ? DSB_MINW_FAST : DSB_MINW_RESOLVE)
 #include "dsb_debug.h"
 
 #define HIP_OK(x)                                                                                    \
@@ -108,7 +127,7 @@ static_assert(sizeof(dsb_rstate_t) <= DSB_STATE_BYTES, "per-read phase state mus
 /* One phase of classify part A (dsb_phase), one lane per read; the read's control state
  * lives in its workspace between launches.  The last phase publishes the read's summary. */
 template <int PH, bool STATS>
-__global__ __launch_bounds__(64) void k_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+__global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 					       const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 					       uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 					       dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
@@ -155,13 +174,14 @@ __global__ __launch_bounds__(64) void k_phase(const dsb_dindex_t *__restrict__ i
 /* One phase of part A with one wavefront per read (dsb_wave.h), one wave per workgroup:
  * fast seeding (FAST0/FAST1), chaining (RESOLVE_*), scoring (DELA).  The last phase
  * publishes the read's summary like k_phase. */
-template <bool STATS>
-__global__ __launch_bounds__(64) void k_wave_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+template <int PH, bool STATS>
+__global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 						    const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 						    uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 						    dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
-						    unsigned long long *__restrict__ gstats, int ph, uint32_t dbg)
+						    unsigned long long *__restrict__ gstats, uint32_t dbg)
 {
+	const int ph = PH;
 	uint32_t t = blockIdx.x;
 	if (t >= n)
 		return;
@@ -190,6 +210,12 @@ __global__ __launch_bounds__(64) void k_wave_phase(const dsb_dindex_t *__restric
 				hset[k] = 0;
 			__syncthreads();
 			dsb_fast_classify_wave(&w, &w.sd[ph - DSB_PH_FAST0], hset);
+		} else if (ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) {
+			uint64_t *hset = (uint64_t *)(base + lay.hset);
+			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
+				hset[k] = 0;
+			__syncthreads();
+			dsb_slow_classify_wave(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem);
 		} else
 			dsb_phase<true>(&w, &f, ph);
 	}
@@ -474,6 +500,28 @@ static phase_kernel_t phase_kernel_at(int ph, bool stats)
 }
 static_assert(DSB_PH_N == 9, "phase dispatch table");
 
+typedef void (*wave_kernel_t)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
+			      const uint32_t *, uint32_t, dsb_read_out_t *, uint32_t *, unsigned long long *, uint32_t);
+template <int PH>
+static wave_kernel_t wave_kernel(bool stats)
+{
+	return stats ? k_wave_phase<PH, true> : k_wave_phase<PH, false>;
+}
+static wave_kernel_t wave_kernel_at(int ph, bool stats)
+{
+	switch (ph) {
+	case DSB_PH_FAST0: return wave_kernel<DSB_PH_FAST0>(stats);
+	case DSB_PH_FAST1: return wave_kernel<DSB_PH_FAST1>(stats);
+	case DSB_PH_RESOLVE_F: return wave_kernel<DSB_PH_RESOLVE_F>(stats);
+	case DSB_PH_SLOW0: return wave_kernel<DSB_PH_SLOW0>(stats);
+	case DSB_PH_SLOW1: return wave_kernel<DSB_PH_SLOW1>(stats);
+	case DSB_PH_RESOLVE_S0: return wave_kernel<DSB_PH_RESOLVE_S0>(stats);
+	case DSB_PH_RESOLVE_S1: return wave_kernel<DSB_PH_RESOLVE_S1>(stats);
+	case DSB_PH_DELA: return wave_kernel<DSB_PH_DELA>(stats);
+	default: return nullptr;
+	}
+}
+
 static float ev_ms(dsb_gpu_dev *g)
 {
 	hipEventRecord(g->ev_b, g->stream);
@@ -530,8 +578,8 @@ static uint32_t wave_phases(void)
 	const char *e = getenv("DSB_WAVE_PHASES");
 	if (e)
 		return (uint32_t)strtoul(e, NULL, 0);
-	return (1u << DSB_PH_FAST0) | (1u << DSB_PH_FAST1) | (1u << DSB_PH_RESOLVE_F) | (1u << DSB_PH_RESOLVE_S0) |
-	       (1u << DSB_PH_RESOLVE_S1) | (1u << DSB_PH_DELA);
+	return (1u << DSB_PH_FAST0) | (1u << DSB_PH_FAST1) | (1u << DSB_PH_RESOLVE_F) | (1u << DSB_PH_SLOW0) |
+	       (1u << DSB_PH_RESOLVE_S0) | (1u << DSB_PH_SLOW1) | (1u << DSB_PH_RESOLVE_S1) | (1u << DSB_PH_DELA);
 }
 
 /* one phase of part A over the reads order[0..m) */
@@ -540,9 +588,9 @@ static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl,
 {
 	hipStream_t s = g->stream;
 	if ((wave_phases() >> ph) & 1)
-		hipLaunchKernelGGL(stats ? k_wave_phase<true> : k_wave_phase<false>, dim3(m), dim3(64), 0, s, g->d, cl,
+		hipLaunchKernelGGL(wave_kernel_at(ph, stats), dim3(m), dim3(64), 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
-				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), ph, wave_dbg());
+				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), wave_dbg());
 	else
 		hipLaunchKernelGGL(phase_kernel_at(ph, stats), dim3((m + 63) / 64), dim3(64), 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
