@@ -16,9 +16,10 @@ index is not available offline) + R = 100k reads per rank.  If data/c1_index.txz
 absent the committed fixture index is used and config.workload says so.
 
 The JSON line carries:
-  roofline     k_classA (the dominant kernel): algorithmic bytes per launch from the work
-               counters of one untimed stats run / its average launch
-               time from HIP events on the library's stream over the timed steps;
+  roofline     the dominant kernel (the phase of classify part A with the largest HIP-event
+               time over the timed steps, on the library's stream): algorithmic bytes per
+               launch from the work counters of one untimed stats run
+               / its average launch time;
                traffic = HBM bytes per launch from the committed PMC profile of this
                workload (profiles/), or null.
   cpu_baseline the reference classifier (oracle/_ref/deSAMBA, built from the reference
@@ -44,7 +45,19 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 METRIC = "long reads classified/sec + Gbases/sec at 1/2/4/8 MI355X; bit-exact taxid match"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
-ST = ["occ", "occ_nib", "mem_search", "sa", "uni", "ref_pos", "getref_b", "anchor", "chain", "ek1", "ek2"]
+# the phase kernels of classify part A (kernels.hip launch_phase)
+KERNEL_OF = {"island": "k_phase<0>", "fast0": "k_wave_phase<1>", "fast1": "k_wave_phase<2>",
+             "resolve_f": "k_wave_phase<3>", "slow0": "k_wave_phase<4>", "resolve_s0": "k_wave_phase<5>",
+             "slow1": "k_wave_phase<6>", "resolve_s1": "k_wave_phase<7>", "delA": "k_wave_phase<8>"}
+
+
+def phase_bytes(c):
+    """Algorithmic HBM bytes of one phase from its work counters:
+    occ checkpoint + nibble bytes, 16 B per MEM-search interval, 8 B per SA sample / unitig /
+    ref_pos entry, 2 bits per reference base unpacked, 56 B per anchor / chain written, the
+    read-hash build bytes, 4 B per hash lookup and 8 B per hash-list node visited."""
+    return (c["occ_nib"] + 16 * c["mem_search"] + 8 * (c["sa"] + c["uni"] + c["ref_pos"]) + c["getref_b"]
+            + 56 * (c["anchor"] + c["chain"]) + c["hash_b"] + 4 * c["lookup"] + 8 * c["node"])
 
 
 def log(*a):
@@ -213,30 +226,34 @@ def main():
     bases_total = batch.n_bases * world * a.steps
     classified = int(counts[1:].sum().item())
 
-    # ---- roofline of k_classA: algorithmic bytes (stats run) / avg HIP-event launch time
-    ms_A = sum(t["ms_classA"] for t in tms) / a.steps
-    launches_A = tms[0]["n_chunks"]
+    # ---- roofline of the dominant kernel: algorithmic bytes (work counters of one untimed
+    # stats run) per launch / its average HIP-event launch time
+    phase_ms = {k: sum(t["ms_phase"][k] for t in tms) / a.steps for k in tms[0]["ms_phase"]}
+    dom = max(phase_ms, key=phase_ms.get)
+    launches = tms[0]["n_chunks"]
     roof = None
     stats = None
     if not a.no_stats:
         ts = batch.run(max_read_l=0, stats=True)
-        sA = ts["stats"]
-        bytes_A = (batch.n_bases + sA["occ_nib"] + 16 * sA["mem_search"] + 8 * (sA["sa"] + sA["uni"] + sA["ref_pos"])
-                   + sA["getref_b"] + 56 * (sA["anchor"] + sA["chain"]))
-        per_launch = bytes_A / launches_A
-        achieved = per_launch / (ms_A / launches_A / 1e3) / 1e9
+        per_phase = {}
+        for ph, c in ts["stats_phase"].items():
+            b = phase_bytes(c) + (batch.n_bases if ph in ("fast0", "slow0") else 0)
+            ms = phase_ms[ph] / launches
+            per_phase[ph] = {"algorithmic_bytes_per_launch": int(b / launches), "avg_launch_ms": round(ms, 3),
+                             "achieved_GBs": round(b / launches / (ms / 1e3) / 1e9, 3) if ms > 0 else None}
+        d = per_phase[dom]
         traffic = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
-            if tj.get("workload") == workload and tj.get("reads") == a.reads:
-                traffic = tj.get("k_classA_hbm_bytes_per_launch")
-        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "kernel": "k_classA",
-                "algorithmic_bytes_per_launch": int(per_launch), "launches_per_step": launches_A,
-                "avg_launch_ms": round(ms_A / launches_A, 3)}
-        stats = {"A": sA, "B": ts["stats_B"]}
+            if tj.get("workload") == workload and tj.get("reads") == a.reads and tj.get("kernel") == KERNEL_OF[dom]:
+                traffic = tj.get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 6), "traffic": traffic, "kernel": KERNEL_OF[dom],
+                "phase": dom, "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
+                "launches_per_step": launches, "avg_launch_ms": d["avg_launch_ms"], "phases": per_phase}
+        stats = {"phases": ts["stats_phase"], "classB": ts["stats_B"]}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -256,7 +273,7 @@ def main():
             "classified_reads": classified,
             "phase_ms": {k: round(sum(t[k] for t in tms) / a.steps, 2)
                          for k in ("ms_encode", "ms_seed", "ms_classA", "ms_classB", "ms_d2h", "ms_total")},
-            "phase_ms_classA": {k: round(sum(t["ms_phase"][k] for t in tms) / a.steps, 2) for k in tms[0]["ms_phase"]},
+            "phase_ms_classA": {k: round(v, 2) for k, v in phase_ms.items()},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

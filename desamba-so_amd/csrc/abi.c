@@ -124,7 +124,7 @@ int dsb_classify_text(void *idx, const char *text, uint64_t text_n, int format, 
 		timing->n_retry = gt.n_retry;
 		timing->n_chunks = gt.n_chunks;
 		timing->seed_positions = gt.seed_positions;
-		for (int k = 0; k < 32; k++) timing->stats[k] = gt.stats[k];
+		for (int k = 0; k < 160; k++) timing->stats[k] = gt.stats[k];
 	}
 	free(ro);
 	free(hits);
@@ -198,7 +198,7 @@ static void copy_timing(dsb_timing_t *t, const dsb_gpu_timing *gt)
 	t->n_retry = gt->n_retry;
 	t->n_chunks = gt->n_chunks;
 	t->seed_positions = gt->seed_positions;
-	for (int k = 0; k < 32; k++) t->stats[k] = gt->stats[k];
+	for (int k = 0; k < 160; k++) t->stats[k] = gt->stats[k];
 }
 
 dsb_batch *dsb_batch_create(void *idx, const char *text, uint64_t text_n, dsb_timing_t *timing)

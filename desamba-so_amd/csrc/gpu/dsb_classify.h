@@ -106,7 +106,11 @@ typedef struct {
 } dsb_read_ws;
 
 enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, DSB_ST_REFPOS,
-       DSB_ST_GETREF_B, DSB_ST_ANCHOR, DSB_ST_CHAIN, DSB_ST_EK1, DSB_ST_EK2, DSB_ST_N };
+       DSB_ST_GETREF_B, DSB_ST_ANCHOR, DSB_ST_CHAIN, DSB_ST_EK1, DSB_ST_EK2,
+       DSB_ST_HASH_B,   /* read 9-mer hash: bytes written/read while building it */
+       DSB_ST_LOOKUP,   /* reference-window k-mer lookups into that hash (4 B head each) */
+       DSB_ST_NODE,     /* hash-list nodes visited by those lookups (8 B each) */
+       DSB_ST_N };
 
 /*
  * Work accounting (stats kernels only; w->stats == 0 otherwise).  The byte figures are the
@@ -1362,6 +1366,7 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 			 * shuffles.  kmer(c) = (OR_k q[c+k] << 2(8-k)) & 0x3ffff is the rolled value. */
 			uint32_t lane = dsb_lane();
 			for (uint32_t k = lane; k <= KEY_MASK; k += DSB_WV) heads[k] = 0xffffffffu;
+			if (w->stats && lane == 0) w->stats[DSB_ST_HASH_B] += 4ull * (KEY_MASK + 1);
 			dsb_wsync();
 			uint32_t n_pos = (uint32_t)(q_len - DSB_S_A_KMER_L + 1);
 			for (uint32_t cb = 0; cb < n_pos; cb += DSB_WV) {
@@ -1386,6 +1391,7 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 					if (hd != 0xffffffffu) tl = tails[key];
 				}
 				if (act) {
+					if (w->stats) w->stats[DSB_ST_HASH_B] += 16;
 					kk[c_pos] = kmer;
 					next[c_pos] = (nxt >= 0) ? cb + (uint32_t)nxt : 0xffffffffu;
 					if (prev < 0) {
@@ -1530,7 +1536,9 @@ DSB_HDN void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const u
 					for (int j = DSB_MAX(4, i - 12); j <= i; j++)
 						kmer |= ((uint64_t)t_str[(int)t_len - DSB_S_A_KMER_L - j] << 16) >> (2 * (i - j));
 				}
+				if (w->stats) w->stats[DSB_ST_LOOKUP]++;
 				for (uint32_t nd = heads[kmer & KEY_MASK]; nd != 0xffffffffu; nd = next[nd]) {
+					if (w->stats) w->stats[DSB_ST_NODE]++;
 					if (isForward ? (kk[nd] != (uint32_t)kmer) : ((uint64_t)kk[nd] != kmer))
 						continue;
 					uint32_t q_pos = nd;

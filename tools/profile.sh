@@ -1,0 +1,14 @@
+#!/bin/bash
+# tools/profile.sh — rocprofv3 evidence for the bench workload (GPU box):
+#   pass 1: kernel trace + stats (per-kernel average durations)
+#   pass 2: FETCH_SIZE, pass 3: WRITE_SIZE (separate passes: TCC slots; no tracing domains)
+# Results land in gpurun_out/prof_*; tools/prof_summary.py condenses them into profiles/.
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$R/gpurun_out
+export TMPDIR=/tmp
+cd /tmp
+B="$R/bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu --no-stats"
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_kt" -o kt -- python3 $B > "$OUT/prof_kt.json" 2> "$OUT/prof_kt.err"
+timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof_fetch" -o pf -- python3 $B > "$OUT/prof_fetch.json" 2> "$OUT/prof_fetch.err"
+timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof_write" -o pw -- python3 $B > "$OUT/prof_write.json" 2> "$OUT/prof_write.err"
