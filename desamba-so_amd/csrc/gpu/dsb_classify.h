@@ -89,6 +89,7 @@ typedef struct {
 	dsb_chain_t *hit; uint32_t n_hit;
 	dsb_chain_t *hit_tmp;
 	dsb_spd_t *sms; uint32_t n_sms;
+	dsb_spd_t *sms_lds;     /* wave scoring: the first DSB_SMS_LDS sms entries live in LDS */
 	uint32_t *hh[2], *ht[2], *hn[2], *hk[2]; /* read 9-mer hash: heads, tails, next, kmer */
 	dsb_sch_t *sch;         /* 256 + 2*400 */
 	uint8_t *win;           /* DSB_WIN_BYTES: sdp_middle ref[2000] and sdp_right/left ref[1000] windows */
@@ -146,22 +147,53 @@ DSB_HD int dsb_exist_bit(const uint64_t *ex, uint32_t k)
 	return (int)((ex[k >> 6] >> (k & 63)) & 1);
 }
 
+/* diagnostics (dbg 256): is [p+lo, p+hi) inside the read's window buffer? */
+DSB_HD int dsb_win_ok(const dsb_read_ws *w, const uint8_t *p, int64_t lo, int64_t hi, int tag)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	if (w->dbg & 256) {
+		int64_t a = (int64_t)(p - w->win) + lo, b = (int64_t)(p - w->win) + hi;
+		if (a < 0 || b > DSB_WIN_BYTES) {
+			printf("[dsb] window access [%ld,%ld) outside [0,%d) tag %d lane %u\n", (long)a, (long)b, DSB_WIN_BYTES,
+			       tag, dsb_lane());
+			return 0;
+		}
+	}
+#endif
+	(void)w; (void)p; (void)lo; (void)hi; (void)tag;
+	return 1;
+}
+
 /* ------------------------------------------------------------------ seeding */
 /* search_exist_kmer_M2, src/cly.c:1066-1155, on precomputed exist bits */
-DSB_HD uint32_t dsb_search_exist(const uint64_t *ex, uint32_t l_kmer_v, dsb_seed_t *seed_v, uint32_t direction)
+/* exist-bit reader keeping the last 64-bit word in a register (the scan revisits it ~20x) */
+typedef struct { const uint64_t *ex; uint32_t wi; uint64_t word; } dsb_bitrd_t;
+DSB_HD int dsb_bit(dsb_bitrd_t *b, uint32_t i)
+{
+	uint32_t wi = i >> 6;
+	if (wi != b->wi) {
+		b->wi = wi;
+		b->word = b->ex[wi];
+	}
+	return (int)((b->word >> (i & 63)) & 1);
+}
+
+DSB_HD uint32_t dsb_search_exist(const uint64_t *ex_, uint32_t l_kmer_v, dsb_seed_t *seed_v, uint32_t direction)
 {
 	uint32_t l_seed_v = 0;
+	dsb_bitrd_t br = {ex_, 0xffffffffu, 0};
+	dsb_bitrd_t *ex = &br;
 	const uint32_t STEP_EK = 3;
 	if (direction == DSB_FORWARD) {
 		for (uint32_t i = STEP_EK - 1; i < l_kmer_v; i += STEP_EK) {
-			if (dsb_exist_bit(ex, i)) {
+			if (dsb_bit(ex, i)) {
 				uint32_t offset = i, len = 1;
 				for (int j = 1; j < (int)STEP_EK; ++j) {
-					if (dsb_exist_bit(ex, i - j)) { offset--; len++; }
+					if (dsb_bit(ex, i - j)) { offset--; len++; }
 					else break;
 				}
 				for (int j = 1; i + j < l_kmer_v; ++j) {
-					if (dsb_exist_bit(ex, i + j)) {
+					if (dsb_bit(ex, i + j)) {
 						len++;
 						if (len > 60) break; /* the i += 50 is overwritten below */
 					} else break;
@@ -174,14 +206,14 @@ DSB_HD uint32_t dsb_search_exist(const uint64_t *ex, uint32_t l_kmer_v, dsb_seed
 		}
 	} else {
 		for (int i = (int)l_kmer_v - (int)STEP_EK; i >= 0; i -= STEP_EK) {
-			if (dsb_exist_bit(ex, (uint32_t)i)) {
+			if (dsb_bit(ex, (uint32_t)i)) {
 				uint32_t offset = i, len = 1;
 				for (int j = 1; j < (int)STEP_EK; ++j) {
-					if (dsb_exist_bit(ex, (uint32_t)(i + j))) { offset++; len++; }
+					if (dsb_bit(ex, (uint32_t)(i + j))) { offset++; len++; }
 					else break;
 				}
 				for (int j = 1; j <= i; ++j) {
-					if (dsb_exist_bit(ex, (uint32_t)(i - j))) {
+					if (dsb_bit(ex, (uint32_t)(i - j))) {
 						len++;
 						if (len > 60) break;
 					} else break;
@@ -1274,6 +1306,8 @@ DSB_HD void dsb_get_ref_win(dsb_read_ws *w, uint8_t *ref_str, uint64_t uni_offse
 	} else {
 		uint32_t lane = dsb_lane();
 		if (w->stats && lane == 0) w->stats[DSB_ST_GETREF_B] += (length + 3) / 4;
+		if (!dsb_win_ok(w, ref_str, 0, length, 1))
+			length = 0;
 		uint64_t b0 = uni_offset >> 2;
 		uint32_t odd = (uint32_t)(uni_offset & 3);
 		for (uint32_t k = lane; k < length; k += DSB_WV) {
@@ -1407,13 +1441,27 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 	return key_len;
 }
 
+/* sparse-DP node i of the current window (LDS-resident prefix for the wave kernel) */
+#define DSB_SMS_LDS 384
+#ifndef DSB_SMS_IN_LDS
+#define DSB_SMS_IN_LDS 0 /* experimental (DSB_LDS=1 path); off: sms entries stay in the workspace */
+#endif
+DSB_HD dsb_spd_t *dsb_sms(dsb_read_ws *w, uint64_t i)
+{
+#if DSB_SMS_IN_LDS
+	return (w->sms_lds && i < DSB_SMS_LDS) ? w->sms_lds + i : w->sms + i;
+#else
+	return w->sms + i;
+#endif
+}
+
 DSB_HD dsb_spd_t *dsb_push_sms(dsb_read_ws *w)
 {
 	if (w->n_sms >= w->cap.sms) {
 		w->overflow |= 16;
 		return 0;
 	}
-	return w->sms + w->n_sms++;
+	return dsb_sms(w, w->n_sms++);
 }
 
 /* MEM_search, src/cly.c:1805-1813 */
@@ -1511,6 +1559,8 @@ DSB_HDN void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const u
 		const uint32_t *heads = w->hh[hslot], *next = w->hn[hslot], *kk = w->hk[hslot];
 		int n_i = (lim - 1) >> 2; /* looked-up positions i = 4m, m = 1..n_i */
 		uint32_t lane = dsb_lane();
+		if (!dsb_win_ok(w, t_str, isForward ? 0 : -51, (int64_t)t_len + 64, 2))
+			return;
 		for (int mb = 0; mb < n_i; mb += DSB_WV) {
 			int m = mb + (int)lane + 1;
 			uint32_t cnt = 0;
@@ -1591,9 +1641,9 @@ DSB_HDN void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const u
 				dsb_wsync();
 				return;
 			}
-			dsb_spd_t *dst = w->sms + w->n_sms + off; /* score is left as the buffer holds it */
-			if (cnt > 0) { dst[0].len = e0.len; dst[0].q_pos = e0.q_pos; dst[0].t_pos = e0.t_pos; }
-			if (cnt > 1) { dst[1].len = e1.len; dst[1].q_pos = e1.q_pos; dst[1].t_pos = e1.t_pos; }
+			uint32_t dst = w->n_sms + off; /* score is left as the buffer holds it */
+			if (cnt > 0) { dsb_spd_t *d = dsb_sms(w, dst); d->len = e0.len; d->q_pos = e0.q_pos; d->t_pos = e0.t_pos; }
+			if (cnt > 1) { dsb_spd_t *d = dsb_sms(w, dst + 1); d->len = e1.len; d->q_pos = e1.q_pos; d->t_pos = e1.t_pos; }
 			if (cnt > 2) { /* rare: more than two matches for one position, walk the list again */
 				uint32_t k = 0;
 				for (uint32_t nd = heads[kmer & KEY_MASK]; nd != 0xffffffffu; nd = next[nd]) {
@@ -1628,7 +1678,7 @@ DSB_HDN void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const u
 						}
 					}
 					if (ok) {
-						if (k >= 2) { dst[k].len = len; dst[k].q_pos = qp; dst[k].t_pos = tp; }
+						if (k >= 2) { dsb_spd_t *d = dsb_sms(w, dst + k); d->len = len; d->q_pos = qp; d->t_pos = tp; }
 						k++;
 					}
 				}
@@ -1671,7 +1721,9 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 					return 0;
 				}
 				dsb_get_ref_win<WAVE>(w, ref, (uint64_t)(int64_t)(pre_refoffset + pre_mch) + t_offset, (uint32_t)total_ref_len);
-				dsb_fill_pattern<WAVE>(ref, total_ref_len, 2000 + 64);
+				/* the reference re-initialises the whole ref[2000]; a forward scan of t_len bytes reads
+				 * at most ref[t_len + 58] (MEM_search bound t_len - i - 1 + OVER_SEARCH past i + 9) */
+				dsb_fill_pattern<WAVE>(ref, total_ref_len, DSB_MIN(total_ref_len + 64, 2000 + 64));
 				dsb_sdp_match<WAVE>(w, pre_a->index_in_read + pre_mch - 8, c_a->index_in_read - 1, q_str, ref,
 					      (uint32_t)total_ref_len, key_len, hslot, (uint32_t)(pre_refoffset + pre_mch), 1);
 				if (w->overflow) return 0;
@@ -1683,7 +1735,7 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 			p->len = c_a->mtch_len - DSB_S_A_KMER_L + 1;
 			if (w->n_sms > 1) {
 				for (uint32_t cs = 1; cs < w->n_sms; cs++) {
-					dsb_spd_t *c_spd = w->sms + cs;
+					dsb_spd_t *c_spd = dsb_sms(w, cs);
 					int max_score = (int)c_spd->len;
 					uint32_t max_q = c_spd->q_pos + DSB_MAX_SMS_OVERLAP;
 					uint32_t max_t = c_spd->t_pos + DSB_MAX_SMS_OVERLAP;
@@ -1692,7 +1744,7 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 					for (int64_t pb = (int64_t)cs - 1; pb >= 0; pb -= (wv ? DSB_WV : 1)) {
 						int64_t ps = pb - (wv ? (int64_t)dsb_lane() : 0);
 						for (int64_t pe = (wv && ps >= 0) ? ps : 0; ps >= pe; ps--) { /* WAVE: one node per lane */
-							dsb_spd_t *c_pre = w->sms + ps;
+							dsb_spd_t *c_pre = dsb_sms(w, ps);
 							int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
 							int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
 							if ((uint32_t)pre_q_ed > max_q) continue; /* int vs uint32 */
@@ -1797,7 +1849,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 				max_search_ref = (uint32_t)(t_length - c_t_offset);
 			max_search_ref = DSB_MIN(600u, max_search_ref);
 			dsb_get_ref_win<WAVE>(w, ref, c_t_offset + t_offset_global, max_search_ref + DSB_OVER_SEARCH);
-			int search_q_ed = (int)w->sms[max_sms_id].q_pos + 1000;
+			int search_q_ed = (int)dsb_sms(w, max_sms_id)->q_pos + 1000;
 			search_q_ed = DSB_MIN(search_q_ed, l_read);                /* int vs uint32: unsigned */
 			int search_q_st = DSB_MAX(search_q_ed - 2000, c_h->q_st - 8); /* idem (H11) */
 			dsb_sdp_match<WAVE>(w, (uint32_t)search_q_st, (uint32_t)search_q_ed, q_str, ref, max_search_ref, key_len, hslot,
@@ -1806,16 +1858,16 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 			c_t_offset += max_search_ref - DSB_S_A_KMER_L - 3;
 			if (w->n_sms == current_sms)
 				break;
-			if (w->sms[current_sms].t_pos > w->sms[max_sms_id].t_pos + 1000)
+			if (dsb_sms(w, current_sms)->t_pos > dsb_sms(w, max_sms_id)->t_pos + 1000)
 				break;
 		}
-		dsb_spd_t *c_sms = w->sms + current_sms++;
+		dsb_spd_t *c_sms = dsb_sms(w, current_sms++);
 		int max_score = (int)c_sms->len;
 		uint32_t max_pre_q = c_sms->q_pos + DSB_MAX_SMS_OVERLAP;
 		uint32_t max_pre_t = c_sms->t_pos + DSB_MAX_SMS_OVERLAP;
 		if (!WAVE || (w->dbg & 4)) {
 			for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
-				dsb_spd_t *c_pre = w->sms + ps;
+				dsb_spd_t *c_pre = dsb_sms(w, ps);
 				int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
 				int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
 				if ((uint32_t)pre_q_ed > max_pre_q) continue; /* int vs uint32 */
@@ -1839,7 +1891,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 				int64_t ps = pb - (int64_t)lane;
 				int cand = INT32_MIN, brk = 0;
 				if (ps >= 0) {
-					dsb_spd_t *c_pre = w->sms + ps;
+					dsb_spd_t *c_pre = dsb_sms(w, ps);
 					int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
 					int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
 					if (!((uint32_t)pre_q_ed > max_pre_q) && !((uint32_t)pre_t_ed > max_pre_t)) {
@@ -1895,11 +1947,11 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 			total_max_score = max_score;
 			max_sms_id = current_sms - 1;
 		}
-		if (c_sms->t_pos > w->sms[max_sms_id].t_pos + 1000)
+		if (c_sms->t_pos > dsb_sms(w, max_sms_id)->t_pos + 1000)
 			break;
 	}
-	c_h->q_ed = w->sms[max_sms_id].q_pos + w->sms[max_sms_id].len + DSB_S_A_KMER_L;
-	c_h->t_ed = w->sms[max_sms_id].t_pos + w->sms[max_sms_id].len + DSB_S_A_KMER_L;
+	c_h->q_ed = dsb_sms(w, max_sms_id)->q_pos + dsb_sms(w, max_sms_id)->len + DSB_S_A_KMER_L;
+	c_h->t_ed = dsb_sms(w, max_sms_id)->t_pos + dsb_sms(w, max_sms_id)->len + DSB_S_A_KMER_L;
 	return total_max_score - 10000;
 }
 
@@ -1946,7 +1998,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 			else
 				dsb_get_ref_win<WAVE>(w, ref, c_t_offset + t_offset_global - max_search_ref - DSB_OVER_SEARCH,
 						      max_search_ref + DSB_OVER_SEARCH);
-			int search_q_st = (int)w->sms[max_sms_id].q_pos - 1000;
+			int search_q_st = (int)dsb_sms(w, max_sms_id)->q_pos - 1000;
 			search_q_st = DSB_MAX(search_q_st, 0);
 			int search_q_ed = DSB_MIN(search_q_st + 2000, c_h->q_st - 1); /* int vs uint32: unsigned */
 			dsb_sdp_match<WAVE>(w, (uint32_t)search_q_st, (uint32_t)search_q_ed, q_str, ref + DSB_OVER_SEARCH, max_search_ref,
@@ -1955,16 +2007,16 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 			c_t_offset = c_t_offset - max_search_ref + DSB_S_A_KMER_L + 3;
 			if (w->n_sms == current_sms)
 				break;
-			if (w->sms[current_sms].t_pos + 1000 < w->sms[max_sms_id].t_pos)
+			if (dsb_sms(w, current_sms)->t_pos + 1000 < dsb_sms(w, max_sms_id)->t_pos)
 				break;
 		}
-		dsb_spd_t *c_sms = w->sms + current_sms++;
+		dsb_spd_t *c_sms = dsb_sms(w, current_sms++);
 		int max_score = (int)c_sms->len;
 		uint32_t min_pre_q = c_sms->q_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
 		uint32_t min_pre_t = c_sms->t_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
 		if (!WAVE || (w->dbg & 4)) {
 			for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
-				dsb_spd_t *c_pre = w->sms + ps;
+				dsb_spd_t *c_pre = dsb_sms(w, ps);
 				if (c_pre->q_pos < min_pre_q) continue;
 				if (c_pre->t_pos < min_pre_t) continue;
 				if (min_pre_t + 600 < c_pre->t_pos) break;
@@ -1986,7 +2038,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 				int64_t ps = pb - (int64_t)lane;
 				int cand = INT32_MIN, brk = 0;
 				if (ps >= 0) {
-					dsb_spd_t *c_pre = w->sms + ps;
+					dsb_spd_t *c_pre = dsb_sms(w, ps);
 					if (!(c_pre->q_pos < min_pre_q) && !(c_pre->t_pos < min_pre_t)) {
 						if (min_pre_t + 600 < c_pre->t_pos)
 							brk = 1;
@@ -2040,11 +2092,11 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 			total_max_score = max_score;
 			max_sms_id = current_sms - 1;
 		}
-		if (c_sms->t_pos + 1000 < w->sms[max_sms_id].t_pos)
+		if (c_sms->t_pos + 1000 < dsb_sms(w, max_sms_id)->t_pos)
 			break;
 	}
-	c_h->q_st = w->sms[max_sms_id].q_pos;
-	c_h->t_st = w->sms[max_sms_id].t_pos;
+	c_h->q_st = dsb_sms(w, max_sms_id)->q_pos;
+	c_h->t_st = dsb_sms(w, max_sms_id)->t_pos;
 	return total_max_score - 10000;
 }
 

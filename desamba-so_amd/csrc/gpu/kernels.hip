@@ -122,6 +122,8 @@ __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ i
 		ex[word] = bits;
 }
 
+#define DSB_WIN_LDS_BYTES ((DSB_WIN_BYTES + 15) & ~15)
+#define DSB_DELA_LDS (DSB_WIN_LDS_BYTES + DSB_SMS_LDS * sizeof(dsb_spd_t))
 static_assert(sizeof(dsb_rstate_t) <= DSB_STATE_BYTES, "per-read phase state must fit its workspace slot");
 
 /* One phase of classify part A (dsb_phase), one lane per read; the read's control state
@@ -201,6 +203,11 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 	if (STATS) {
 		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
 		w.stats = st;
+	}
+	if (PH == DSB_PH_DELA && (dbg & 512)) { /* scoring: reference windows and the sparse-DP prefix in LDS */
+		extern __shared__ uint8_t dsb_lds[];
+		w.win = dsb_lds;
+		w.sms_lds = (dsb_spd_t *)(dsb_lds + DSB_WIN_LDS_BYTES);
 	}
 	int active = dsb_phase_active(&w, &f, ph);
 	if (active) {
@@ -566,10 +573,15 @@ static uint64_t seed_words(const std::vector<uint32_t> &len, uint64_t cb, const 
 	return tw;
 }
 
+/* diagnostics / experiments: DSB_WAVE_DBG bits (dsb_classify.h), DSB_LDS=1 -> bit 512 */
 static uint32_t wave_dbg(void)
 {
 	const char *e = getenv("DSB_WAVE_DBG");
-	return e ? (uint32_t)strtoul(e, NULL, 0) : 0;
+	uint32_t d = e ? (uint32_t)strtoul(e, NULL, 0) : 0;
+	const char *l = getenv("DSB_LDS");
+	if (l && atoi(l))
+		d |= 512;
+	return d;
 }
 
 /* phases run with one wavefront per read (DSB_WAVE_PHASES overrides, for diagnostics) */
@@ -588,7 +600,8 @@ static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl,
 {
 	hipStream_t s = g->stream;
 	if ((wave_phases() >> ph) & 1)
-		hipLaunchKernelGGL(wave_kernel_at(ph, stats), dim3(m), dim3(64), 0, s, g->d, cl,
+		hipLaunchKernelGGL(wave_kernel_at(ph, stats), dim3(m), dim3(64),
+				   (ph == DSB_PH_DELA && (wave_dbg() & 512)) ? DSB_DELA_LDS : 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
 				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), wave_dbg());
 	else

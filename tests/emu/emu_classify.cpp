@@ -91,6 +91,15 @@ int main(int argc, char **argv)
 					}
 				}
 			}
+			static uint8_t lds_win[DSB_WIN_BYTES];
+			static dsb_spd_t lds_sms[DSB_SMS_LDS];
+			if (getenv("EMU_LDS")) { /* the scoring kernel's LDS layout (separate window / sms prefix) */
+				int fill = (int)strtol(getenv("EMU_LDS"), 0, 0); /* garbage left by other workgroups */
+				memset(lds_win, fill, sizeof(lds_win));
+				memset(lds_sms, fill, sizeof(lds_sms));
+				w.win = lds_win;
+				w.sms_lds = lds_sms;
+			}
 			if (getenv("EMU_WAVE")) { /* the wave-cooperative code paths, as a one-lane wave */
 				dsb_rflags_t f = {0, 0, 0, 0};
 				uint64_t *hset = (uint64_t *)(arena.data() + lay.hset);
