@@ -21,7 +21,11 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define DSB_HD __host__ __device__ __forceinline__
+#if defined(DSB_HDN_INLINE) && DSB_HDN_INLINE
+#define DSB_HDN __host__ __device__ __forceinline__
+#else
 #define DSB_HDN __host__ __device__ __noinline__
+#endif
 #else
 #define DSB_HD static inline
 #define DSB_HDN static

@@ -27,8 +27,8 @@
 #include "dsb_gpu.h"
 
 /* minimum waves per SIMD requested from the register allocator (spills beyond) */
-/* measured on MI355X (C1 workload): fast seeding is fastest at 2 waves/SIMD, the scoring
- * phase at 4, the lane-per-read phases at 2 (profiles/) */
+/* measured on MI355X (C1 workload, fully inlined phase kernels): fast/slow seeding is fastest
+ * at 2 waves/SIMD, the scoring phase at 8, the lane-per-read phases at 2 */
 #ifndef DSB_MINW_LANE
 #define DSB_MINW_LANE 2
 #endif
@@ -36,7 +36,7 @@
 #define DSB_MINW_FAST 2
 #endif
 #ifndef DSB_MINW_DELA
-#define DSB_MINW_DELA 4
+#define DSB_MINW_DELA 8
 #endif
 #ifndef DSB_MINW_RESOLVE
 #define DSB_MINW_RESOLVE 4
