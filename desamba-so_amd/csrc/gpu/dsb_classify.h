@@ -111,7 +111,18 @@ enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, 
        DSB_ST_HASH_B,   /* read 9-mer hash: bytes written/read while building it */
        DSB_ST_LOOKUP,   /* reference-window k-mer lookups into that hash (4 B head each) */
        DSB_ST_NODE,     /* hash-list nodes visited by those lookups (8 B each) */
+       DSB_ST_T_MEM,    /* shader clocks inside bwt_MEM_search (stats kernels only) */
+       DSB_ST_T_MAP,    /* shader clocks inside map_seed (stats kernels only) */
        DSB_ST_N };
+
+DSB_HD uint64_t dsb_clock(void)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+	return __builtin_amdgcn_s_memtime();
+#else
+	return 0;
+#endif
+}
 
 /*
  * Work accounting (stats kernels only; w->stats == 0 otherwise).  The byte figures are the
@@ -702,8 +713,10 @@ DSB_HD int dsb_fast_seed(dsb_read_ws *w, const dsb_sdir_t *s_d, uint32_t ci, SET
 		uint64_t kmer = dsb_kmer_at(bin_read + kmer_index, l_ek, ix->single_base_max);
 		uint64_t prefixValue = kmer & DSB_PRE_IDX_MASK;
 		int string_index = kmer_index + l_ek - 1;
+		uint64_t t0 = w->stats ? dsb_clock() : 0;
 		int n_m = dsb_mem_search(w, bin_read + string_index, prefixValue, DSB_MEM_SEARCH_FAST,
 					 DSB_MIN_MEM_LEN_FAST - 1, string_index, sp_set, m_r);
+		if (w->stats) w->stats[DSB_ST_T_MEM] += dsb_clock() - t0;
 		if (n_m == 0) {
 			j -= 2;
 			continue;
@@ -712,7 +725,9 @@ DSB_HD int dsb_fast_seed(dsb_read_ws *w, const dsb_sdir_t *s_d, uint32_t ci, SET
 		int max_score = 0;
 		for (int k = 0; k < n_m; k++) {
 			m_r[k].read_offset = string_index - m_r[k].match_len;
+			uint64_t t1 = w->stats ? dsb_clock() : 0;
 			int c_score = dsb_map_seed(w, m_r + k, &s_i);
+			if (w->stats) w->stats[DSB_ST_T_MAP] += dsb_clock() - t1;
 			max_score = DSB_MAX(c_score, max_score);
 		}
 		if (w->overflow)

@@ -201,6 +201,9 @@ DSB_HD int32_t dsb_lv_extd(uint8_t *ref, int32_t ref_length, uint8_t *query, int
 	ref[ref_length] = '#';
 	query[query_length] = '$';
 	int32_t best_score = query_length;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
 	for (int i = -DSB_LV_ERROR - 1; i <= DSB_LV_ERROR + 1; i++) {
 		mn[i] = -1;
 		ed[i] = (i > 0) ? i : -i;
@@ -208,6 +211,9 @@ DSB_HD int32_t dsb_lv_extd(uint8_t *ref, int32_t ref_length, uint8_t *query, int
 	/* mn[LV_ERROR+2] is read (never used) in the reference: keep an initialised slot */
 	mn[DSB_LV_ERROR + 2] = -1;
 	ed[DSB_LV_ERROR + 2] = DSB_LV_ERROR + 2;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
 	for (int i = 0; i <= DSB_LV_ERROR; i++) {
 		prev_mn = -1;
 		cur_mn = i - 1;
@@ -215,6 +221,9 @@ DSB_HD int32_t dsb_lv_extd(uint8_t *ref, int32_t ref_length, uint8_t *query, int
 		prev_ed = i + 1;
 		cur_ed = i;
 		next_ed = ed[-i + 1];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
 		for (int j = -i; j <= DSB_LV_ERROR; j++) {
 			if (cur_mn + j < ref_length - 1) {
 				int MAX_mn_ed = cur_mn + 1 - cur_ed;

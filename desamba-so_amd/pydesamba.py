@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libdesamba.so")
 FMT_SAM, FMT_SAM_FULL, FMT_DES, FMT_DES_FULL = 1, 2, 3, 4
 PHASES = ["island", "fast0", "fast1", "resolve_f", "slow0", "resolve_s0", "slow1", "resolve_s1", "delA"]
 ST_NAMES = ["occ", "occ_nib", "mem_search", "sa", "uni", "ref_pos", "getref_b", "anchor", "chain", "ek1", "ek2",
-            "hash_b", "lookup", "node"]
+            "hash_b", "lookup", "node", "t_mem", "t_map"]
 
 
 class Timing(C.Structure):

@@ -137,7 +137,7 @@ int main(int argc, char **argv)
 	fwrite(out.s, 1, out.l, stdout);
 	if (stats) {
 		fprintf(stderr, "reads %lu retries %lu\n", (unsigned long)reads.n, (unsigned long)n_retry);
-		const char *nm[DSB_ST_N] = {"occ", "occ_nib", "memsearch", "sa", "uni", "refpos", "getref_b", "anchor", "chain", "ek1", "ek2", "hash_b", "lookup", "node"};
+		const char *nm[DSB_ST_N] = {"occ", "occ_nib", "memsearch", "sa", "uni", "refpos", "getref_b", "anchor", "chain", "ek1", "ek2", "hash_b", "lookup", "node", "t_mem", "t_map"};
 		for (int k = 0; k < DSB_ST_N; k++) fprintf(stderr, "%s %lu\n", nm[k], (unsigned long)st[k]);
 	}
 	return 0;
