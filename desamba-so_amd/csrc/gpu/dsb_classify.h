@@ -189,51 +189,95 @@ DSB_HD int dsb_bit(dsb_bitrd_t *b, uint32_t i)
 	return (int)((b->word >> (i & 63)) & 1);
 }
 
+/* positions p with p % 3 == rho inside a 64-bit word (64 % 3 == 1) */
+DSB_HD uint64_t dsb_mask3(uint32_t rho)
+{
+	const uint64_t M0 = 0x9249249249249249ull; /* bits 0, 3, ..., 63 */
+	return rho == 0 ? M0 : (rho == 1 ? (M0 << 1) : (M0 << 2));
+}
+/* smallest p >= i with p == i (mod 3), p < n and exist bit p set; n if none */
+DSB_HD uint32_t dsb_next_set3(const uint64_t *ex, uint32_t i, uint32_t n)
+{
+	uint32_t r3 = i % 3;
+	while (i < n) {
+		uint32_t w = i >> 6, b = i & 63;
+		uint64_t bits = ex[w] & dsb_mask3((r3 + 3 - (w << 6) % 3) % 3) & (~0ull << b);
+		if (bits) {
+			uint32_t p = (w << 6) + (uint32_t)__builtin_ctzll(bits);
+			return p < n ? p : n;
+		}
+		uint32_t nx = (w + 1) << 6;
+		i = nx + (r3 + 3 - nx % 3) % 3;
+	}
+	return n;
+}
+/* largest p <= i with p == i (mod 3) and exist bit p set; -1 if none */
+DSB_HD int dsb_prev_set3(const uint64_t *ex, int i)
+{
+	uint32_t r3 = (uint32_t)i % 3;
+	while (i >= 0) {
+		uint32_t w = (uint32_t)i >> 6, b = (uint32_t)i & 63;
+		uint64_t upto = (b == 63) ? ~0ull : ((2ull << b) - 1);
+		uint64_t bits = ex[w] & dsb_mask3((r3 + 3 - (w << 6) % 3) % 3) & upto;
+		if (bits)
+			return (int)((w << 6) + 63 - (uint32_t)__builtin_clzll(bits));
+		if (w == 0)
+			return -1;
+		int last = (int)(w << 6) - 1;
+		i = last - (int)(((uint32_t)last % 3 + 3 - r3) % 3);
+	}
+	return -1;
+}
+
 DSB_HD uint32_t dsb_search_exist(const uint64_t *ex_, uint32_t l_kmer_v, dsb_seed_t *seed_v, uint32_t direction)
 {
 	uint32_t l_seed_v = 0;
 	dsb_bitrd_t br = {ex_, 0xffffffffu, 0};
 	dsb_bitrd_t *ex = &br;
 	const uint32_t STEP_EK = 3;
+	/* the candidate positions (every 3rd k-mer, restarting after each seed) are found a word
+	 * at a time (dsb_next_set3 / dsb_prev_set3) instead of bit by bit */
 	if (direction == DSB_FORWARD) {
 		for (uint32_t i = STEP_EK - 1; i < l_kmer_v; i += STEP_EK) {
-			if (dsb_bit(ex, i)) {
-				uint32_t offset = i, len = 1;
-				for (int j = 1; j < (int)STEP_EK; ++j) {
-					if (dsb_bit(ex, i - j)) { offset--; len++; }
-					else break;
-				}
-				for (int j = 1; i + j < l_kmer_v; ++j) {
-					if (dsb_bit(ex, i + j)) {
-						len++;
-						if (len > 60) break; /* the i += 50 is overwritten below */
-					} else break;
-				}
-				seed_v[l_seed_v].offset = offset;
-				seed_v[l_seed_v].len = len;
-				l_seed_v++;
-				i = offset + len;
+			i = dsb_next_set3(ex_, i, l_kmer_v);
+			if (i >= l_kmer_v)
+				break;
+			uint32_t offset = i, len = 1;
+			for (int j = 1; j < (int)STEP_EK; ++j) {
+				if (dsb_bit(ex, i - j)) { offset--; len++; }
+				else break;
 			}
+			for (int j = 1; i + j < l_kmer_v; ++j) {
+				if (dsb_bit(ex, i + j)) {
+					len++;
+					if (len > 60) break; /* the i += 50 is overwritten below */
+				} else break;
+			}
+			seed_v[l_seed_v].offset = offset;
+			seed_v[l_seed_v].len = len;
+			l_seed_v++;
+			i = offset + len;
 		}
 	} else {
 		for (int i = (int)l_kmer_v - (int)STEP_EK; i >= 0; i -= STEP_EK) {
-			if (dsb_bit(ex, (uint32_t)i)) {
-				uint32_t offset = i, len = 1;
-				for (int j = 1; j < (int)STEP_EK; ++j) {
-					if (dsb_bit(ex, (uint32_t)(i + j))) { offset++; len++; }
-					else break;
-				}
-				for (int j = 1; j <= i; ++j) {
-					if (dsb_bit(ex, (uint32_t)(i - j))) {
-						len++;
-						if (len > 60) break;
-					} else break;
-				}
-				seed_v[l_seed_v].offset = offset - len + 1;
-				seed_v[l_seed_v].len = len;
-				l_seed_v++;
-				i = (int)(offset - len);
+			i = dsb_prev_set3(ex_, i);
+			if (i < 0)
+				break;
+			uint32_t offset = i, len = 1;
+			for (int j = 1; j < (int)STEP_EK; ++j) {
+				if (dsb_bit(ex, (uint32_t)(i + j))) { offset++; len++; }
+				else break;
 			}
+			for (int j = 1; j <= i; ++j) {
+				if (dsb_bit(ex, (uint32_t)(i - j))) {
+					len++;
+					if (len > 60) break;
+				} else break;
+			}
+			seed_v[l_seed_v].offset = offset - len + 1;
+			seed_v[l_seed_v].len = len;
+			l_seed_v++;
+			i = (int)(offset - len);
 		}
 	}
 	return l_seed_v;
