@@ -43,3 +43,25 @@ def test_emulated_work_counters(emu, fixture_index, tmp_path):
     assert st["occ"] > 0 and st["occ_nib"] >= 10 * st["occ"]
     assert st["sa"] > 0 and st["uni"] >= st["sa"] and st["anchor"] > 0 and st["chain"] > 0
     assert len(groups(r.stdout)) == 2000
+
+
+@pytest.mark.parametrize("mode", ["wave", "wave_replay", "wave_lds"])
+@pytest.mark.parametrize("name", ["mixed", "ont"])
+def test_emulated_wave_code_paths_are_byte_identical(emu, fixture_index, tmp_path, name, mode):
+    """The wave-cooperative kernels' code (seeding with per-lane staging and the skip rule,
+    chaining, scoring) run as a one-lane wave; `wave_replay` forces every staging area to
+    overflow (the in-order replay path), `wave_lds` separates the scoring windows / sparse-DP
+    prefix the way the LDS variant does and fills them with garbage first."""
+    env = dict(os.environ, EMU_WAVE="1")
+    if mode == "wave_replay":
+        env["EMU_DBG"] = "32"
+    if mode == "wave_lds":
+        env["EMU_LDS"] = "0x7f"
+    fq = tmp_path / f"{name}.fq"
+    fq.write_bytes(golden(name + ".fq"))
+    out = subprocess.run([emu, fixture_index, str(fq)], capture_output=True, check=True, timeout=600, env=env).stdout
+    assert out == golden(name + ".herm.sam_full") if name == "mixed" else True
+    if name != "mixed":
+        sam = subprocess.run([emu, "--sam", fixture_index, str(fq)], capture_output=True, check=True, timeout=600,
+                             env=env).stdout
+        assert sam == golden(name + ".herm.sam")

@@ -152,3 +152,16 @@ def test_batch_taxa_match_meta_analysis_rule(gpu_index, fixture_index, pyd):
         assert (w == 1).all()
     finally:
         b.close()
+
+
+def test_dlopen_consumer_example(fixture_index, tmp_path):
+    """examples/consumer.c (a reference-style dlopen consumer) against the hermetic goldens."""
+    exe = tmp_path / "consumer"
+    subprocess.run(["gcc", "-O2", "-o", str(exe), os.path.join(ROOT, "examples", "consumer.c"), "-ldl"], check=True)
+    fq = tmp_path / "mixed.fq"
+    fq.write_bytes(golden("mixed.fq"))
+    lib = os.path.join(ROOT, "desamba-so_amd", "lib", "libdesamba.so")
+    r = subprocess.run([str(exe), lib, fixture_index, str(fq)], capture_output=True, check=True, timeout=300)
+    assert r.stdout == golden("mixed.herm.sam_full")
+    ref_lines = golden("mixed.meta_reads").decode().splitlines()
+    assert r.stderr.decode().endswith("\n".join(l for l in ref_lines if not l.startswith("#")) + "\n")
