@@ -172,15 +172,21 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    os.environ["DSB_DEVICE"] = str(local)
     import torch
     assert torch.cuda.is_available(), "bench.py needs an MI355X"
+    # one process per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share devices
+    local = local % max(1, torch.cuda.device_count())
+    os.environ["DSB_DEVICE"] = str(local)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("DSB_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     import pydesamba
     import shard
@@ -199,12 +205,13 @@ def main():
     log(f"rank {rank}: {batch.n_reads} reads / {batch.n_bases / 1e6:.1f} Mbp resident in HBM "
         f"(parse+upload {batch.upload['ms_h2d']:.0f} ms)")
     n_tax = idx.max_tid() + 1
-    counts = torch.zeros(n_tax, dtype=torch.int64, device="cuda")
+    cdev = "cuda" if (dist is None or dist.get_backend() == "nccl") else "cpu"
+    counts = torch.zeros(n_tax, dtype=torch.int64, device=cdev)
 
     def step():
         tm = batch.run(max_read_l=0)
         tid, _ = batch.taxa(0)
-        counts.copy_(shard.reduce_counts(shard.taxon_counts(tid, None, n_tax), "cuda"))
+        counts.copy_(shard.reduce_counts(shard.taxon_counts(tid, None, n_tax), cdev))
         return tm
 
     for _ in range(a.warmup):
@@ -218,7 +225,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
@@ -268,7 +275,7 @@ def main():
             "data": "synthetic ONT reads (tools/simulate.py, lognormal mean 8 kb, 5-15% error) from a synthetic reference",
             "config": {"workload": workload, "reads_per_rank": batch.n_reads, "mbases_per_rank": round(batch.n_bases / 1e6, 2),
                        "mean_len": a.mean_len, "parallelism": f"reads sharded over {world} GPU(s), index replicated",
-                       "taxon_reduce": "all_reduce(nccl)" if world > 1 else "none"},
+                       "taxon_reduce": f"all_reduce({dist.get_backend()})" if world > 1 else "none"},
             "gbases_per_s": round(bases_total / elapsed / 1e9, 4),
             "classified_reads": classified,
             "phase_ms": {k: round(sum(t[k] for t in tms) / a.steps, 2)

@@ -809,13 +809,15 @@ DSB_HDN void dsb_fast_classify(dsb_read_ws *w, const dsb_sdir_t *s_d)
 }
 
 /*
- * fast_classify with one wavefront per read: the seeds of the vector are taken 64 at a time,
- * one per lane.  Each lane runs its seed into a private staging area (anc_tmp, S anchors per
- * lane) with its own hashed sp_set; the reference's `ci++` (skip the seed after one that
- * scored > 512) is resolved over the group in seed order, and the kept anchors are compacted
- * into the anchor vector in seed order (prefix sum).  A group in which some lane overflowed
- * its staging area is replayed seed by seed in order.  hset: DSB_HSET_SLOTS x DSB_WV slots,
- * lane-interleaved, zeroed by the caller.
+ * fast_classify with one wavefront per read.  Only `top` seeds do work, so their indices are
+ * first compacted (ballot + prefix, in seed order) and handed out 64 at a time, one per lane.
+ * Each lane runs its seed into a private staging area (anc_tmp, S anchors per lane) with its
+ * own hashed sp_set.  The reference's `ci++` (src/cly.c:1526: after a seed scoring > 512 the
+ * next seed index is skipped) is replayed in order over the group: a top seed is skipped iff
+ * the previously processed seed triggered and sits immediately before it.  Kept anchors are
+ * compacted into the anchor vector in seed order (prefix sum).  A group in which some lane
+ * overflowed its staging area is replayed seed by seed in order.  hset: DSB_HSET_SLOTS x
+ * DSB_WV slots, lane-interleaved, zeroed by the caller; the top list lives in w->sidx.
  */
 DSB_HDN void dsb_fast_classify_wave(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset)
 {
@@ -824,11 +826,26 @@ DSB_HDN void dsb_fast_classify_wave(dsb_read_ws *w, const dsb_sdir_t *s_d, uint6
 	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV; /* dbg 32: tiny staging (tests the replay) */
 	dsb_anchor_t *stg = w->anc_tmp + (uint64_t)lane * S;
 	dsb_hset_t hs = {hset + lane, DSB_WV, 0, 0, 500};
-	int carry = 0;
+	/* ---- top seeds, in order */
+	uint32_t *tix = w->sidx;
+	uint32_t m = 0;
 	for (uint32_t gb = 0; gb < n_sv; gb += DSB_WV) {
 		uint32_t ci = gb + lane;
-		uint32_t gn = DSB_MIN((uint32_t)DSB_WV, n_sv - gb);
-		int act = ci < n_sv && w->seeds[s_d->seed_off + ci].top != 0;
+		int t = ci < n_sv && w->seeds[s_d->seed_off + ci].top != 0;
+		uint64_t bm = dsb_wballot(t);
+		uint64_t below = (lane == 0) ? 0 : (bm & (~0ull >> (64 - lane)));
+		if (t)
+			tix[m + (uint32_t)__builtin_popcountll(below)] = ci;
+		m += (uint32_t)__builtin_popcountll(bm);
+	}
+	dsb_wsync();
+	int last_trig = 0;     /* the previously processed seed triggered the skip */
+	uint32_t last_ci = 0;  /* ... and its index */
+	for (uint32_t gb = 0; gb < m; gb += DSB_WV) {
+		uint32_t k = gb + lane;
+		uint32_t gn = DSB_MIN((uint32_t)DSB_WV, m - gb);
+		int act = k < m;
+		uint32_t ci = act ? tix[k] : 0;
 		int trig = 0, ovf = 0;
 		uint32_t cnt = 0;
 		if (act) {
@@ -846,18 +863,28 @@ DSB_HDN void dsb_fast_classify_wave(dsb_read_ws *w, const dsb_sdir_t *s_d, uint6
 			w->cap.anc = cap0;
 			w->overflow = of0;
 		}
-		/* src/cly.c:1535 `ci++`: a seed is skipped when the previous (processed) one triggered */
 		uint64_t tm = dsb_wballot(act && trig);
 		uint64_t om = dsb_wballot(act && ovf); /* an overflowed lane's trigger is not known yet */
+		/* skips over the group in order (lanes' seed indices via shuffles) */
 		uint64_t skipm = 0;
-		int carry_in = carry, prev = carry;
-		for (uint32_t k = 0; k < gn; k++) {
-			if (prev)
-				skipm |= 1ull << k;
-			prev = !prev && ((tm >> k) & 1);
+		int lt = last_trig;
+		uint32_t lc = last_ci;
+		int unknown = 0;
+		for (uint32_t q = 0; q < gn; q++) {
+			uint32_t cq = (uint32_t)dsb_wshfl((int)ci, (int)q);
+			if (lt && cq == lc + 1) {
+				skipm |= 1ull << q;
+				lt = 0;
+				continue;
+			}
+			if ((om >> q) & 1)
+				unknown = 1;
+			lt = (int)((tm >> q) & 1);
+			lc = cq;
 		}
-		carry = prev;
-		if ((om & ~skipm) == 0) {
+		if (!unknown) {
+			last_trig = lt;
+			last_ci = lc;
 			if ((skipm >> lane) & 1)
 				cnt = 0;
 			uint32_t tot, off = dsb_wscan(cnt, &tot);
@@ -866,41 +893,38 @@ DSB_HDN void dsb_fast_classify_wave(dsb_read_ws *w, const dsb_sdir_t *s_d, uint6
 				dsb_wsync();
 				return;
 			}
-			for (uint32_t k = 0; k < cnt; k++)
-				w->anc[w->n_anc + off + k] = stg[k];
+			for (uint32_t e = 0; e < cnt; e++)
+				w->anc[w->n_anc + off + e] = stg[e];
 			w->n_anc += tot;
 		} else { /* seed by seed, in order, deciding the skips as the reference does */
-			prev = carry_in;
-			for (uint32_t k = 0; k < gn; k++) {
-				uint32_t ck = gb + k;
-				if (prev) {
-					prev = 0;
+			for (uint32_t q = 0; q < gn; q++) {
+				uint32_t cq = (uint32_t)dsb_wshfl((int)ci, (int)q);
+				if (last_trig && cq == last_ci + 1) {
+					last_trig = 0;
 					continue;
 				}
-				if (w->seeds[s_d->seed_off + ck].top == 0)
-					continue;
-				if ((om >> k) & 1) { /* replay on every lane, straight into the anchor vector */
-					prev = dsb_fast_seed(w, s_d, ck, &hs);
+				if ((om >> q) & 1) { /* replay on every lane, straight into the anchor vector */
+					last_trig = dsb_fast_seed(w, s_d, cq, &hs);
 					if (w->overflow) {
 						dsb_wsync();
 						return;
 					}
 				} else {
-					prev = (int)((tm >> k) & 1);
-					uint32_t kc = (uint32_t)dsb_wshfl((int)cnt, (int)k);
+					last_trig = (int)((tm >> q) & 1);
+					uint32_t kc = (uint32_t)dsb_wshfl((int)cnt, (int)q);
 					if (w->n_anc + kc > w->cap.anc) {
 						w->overflow |= 1;
 						dsb_wsync();
 						return;
 					}
-					const dsb_anchor_t *src = w->anc_tmp + (uint64_t)k * S;
+					const dsb_anchor_t *src = w->anc_tmp + (uint64_t)q * S;
 					for (uint32_t e = lane; e < kc; e += DSB_WV)
 						w->anc[w->n_anc + e] = src[e];
 					w->n_anc += kc;
 				}
+				last_ci = cq;
 				dsb_wsync();
 			}
-			carry = prev;
 		}
 		dsb_wsync();
 	}
