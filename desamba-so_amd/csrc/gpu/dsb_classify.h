@@ -11,6 +11,18 @@
 #include "dsb_core.h"
 #include "dsb_wave.h"
 
+/* Sequential variants of the wave loops (w->dbg bits 1, 2, 4, 8, 64) exist for the host
+ * emulation and diagnostics builds only; device builds compile them out (-DDSB_WAVE_DIAG=1
+ * keeps them). */
+#ifndef DSB_WAVE_DIAG
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DSB_WAVE_DIAG 0
+#else
+#define DSB_WAVE_DIAG 1
+#endif
+#endif
+#define DSB_SEQ(w, bit) (DSB_WAVE_DIAG && ((w)->dbg & (bit)))
+
 /* ------------------------------------------------------------------ per-read types */
 typedef struct { uint32_t offset, len; uint8_t top, p0, p1, p2; } dsb_seed_t; /* CLY_seed, cly.h:27-32 */
 
@@ -161,7 +173,7 @@ DSB_HD int dsb_exist_bit(const uint64_t *ex, uint32_t k)
 /* diagnostics (dbg 256): is [p+lo, p+hi) inside the read's window buffer? */
 DSB_HD int dsb_win_ok(const dsb_read_ws *w, const uint8_t *p, int64_t lo, int64_t hi, int tag)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && DSB_WAVE_DIAG
 	if (w->dbg & 256) {
 		int64_t a = (int64_t)(p - w->win) + lo, b = (int64_t)(p - w->win) + hi;
 		if (a < 0 || b > DSB_WIN_BYTES) {
@@ -1159,7 +1171,7 @@ DSB_HD void dsb_sort_anchors(dsb_read_ws *w)
 {
 	uint32_t n = w->n_anc;
 	dsb_anchor_t *A = w->anc;
-	if (!WAVE || (w->dbg & 64)) {
+	if (!WAVE || DSB_SEQ(w, 64)) {
 		uint32_t *idx = w->sidx, *tmp = w->stmp;
 		for (uint32_t k = 0; k < n; k++) idx[k] = k;
 		dsb_msort(idx, tmp, n, [A](uint32_t ia, uint32_t ib) -> int { return dsb_anchor_cmp(A + ia, A + ib); });
@@ -1231,7 +1243,7 @@ DSB_HDN void dsb_chain_insert_M3(dsb_read_ws *w)
 			anchor_max_score = c_a->score;
 			uint32_t max_t = c_a->ref_offset + 3;
 			uint32_t max_q = c_a->index_in_read + 3;
-			if (!WAVE || (w->dbg & 64)) {
+			if (!WAVE || DSB_SEQ(w, 64)) {
 				for (int64_t pi = (int64_t)ca - 1; pi >= (int64_t)chr_st; pi--) {
 					dsb_anchor_t *pre = A + pi;
 					if (pre->index_in_read + pre->mtch_len > max_q) continue;
@@ -1384,7 +1396,7 @@ DSB_HDN void dsb_resolve_tree(dsb_read_ws *w)
 template <bool WAVE>
 DSB_HD void dsb_get_ref_win(dsb_read_ws *w, uint8_t *ref_str, uint64_t uni_offset, uint32_t length)
 {
-	if (!WAVE || (w->dbg & 8)) {
+	if (!WAVE || DSB_SEQ(w, 8)) {
 		dsb_get_ref_w(w, ref_str, uni_offset, length, 1);
 	} else {
 		uint32_t lane = dsb_lane();
@@ -1464,7 +1476,7 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 		int h = (c_dir == 2) ? 0 : 1;
 		uint32_t *heads = w->hh[h], *tails = w->ht[h], *next = w->hn[h], *kk = w->hk[h];
 		const uint8_t *q = w->bin + (csd->strand ? w->L : 0);
-		if (!WAVE || (w->dbg & 1)) {
+		if (!WAVE || DSB_SEQ(w, 1)) {
 			for (uint32_t k = 0; k <= KEY_MASK; k++) heads[k] = 0xffffffffu;
 			uint32_t kmer = 0;
 			for (int k = 0; k < DSB_S_A_KMER_L - 1; k++) kmer = (kmer << 2) | q[k];
@@ -1548,14 +1560,45 @@ DSB_HD dsb_spd_t *dsb_push_sms(dsb_read_ws *w)
 }
 
 /* MEM_search, src/cly.c:1805-1813 */
+/* 8 bytes at p (any alignment) from the two aligned words covering them; may read up to 15
+ * bytes past p, which stay inside the read's workspace arena (guards, or the next region). */
+DSB_HD uint64_t dsb_ld8u(const uint8_t *p)
+{
+	uintptr_t a = (uintptr_t)p;
+	const uint64_t *b = (const uint64_t *)(a & ~(uintptr_t)7);
+	uint32_t sh = (uint32_t)(a & 7) * 8;
+	uint64_t lo = b[0];
+	if (!sh)
+		return lo;
+	return (lo >> sh) | (b[1] << (64 - sh));
+}
+
+/* MEM_search: the byte loop `len < max && *q++ == *t++` (or `*q-- == *t--`) compared 8 bytes
+ * per step: the first differing byte is the lowest (forward) / highest (backward) set byte of
+ * the XOR.  Same result as the byte loop for every max >= 0. */
 DSB_HD int dsb_MEM_search(const uint8_t *q, const uint8_t *t, int forward, int max)
 {
 	int len = 0;
-	if (forward)
-		for (; len < max && *q++ == *t++; len++);
-	else
-		for (; len < max && *q-- == *t--; len++);
-	return len;
+	if (forward) {
+		while (len < max) {
+			uint64_t x = dsb_ld8u(q + len) ^ dsb_ld8u(t + len);
+			if (x) {
+				len += __builtin_ctzll(x) >> 3;
+				return DSB_MIN(len, max);
+			}
+			len += 8;
+		}
+	} else {
+		while (len < max) {
+			uint64_t x = dsb_ld8u(q - len - 7) ^ dsb_ld8u(t - len - 7);
+			if (x) {
+				len += __builtin_clzll(x) >> 3;
+				return DSB_MIN(len, max);
+			}
+			len += 8;
+		}
+	}
+	return max > 0 ? max : 0;
 }
 
 /* sdp_match, src/cly.c:2330-2435.  q_str: read buffer; t_str: reference window.
@@ -1565,7 +1608,7 @@ template <bool WAVE>
 DSB_HDN void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const uint8_t *q_str, const uint8_t *t_str,
 			    uint32_t t_len, int key_len, int hslot, uint32_t t_st, int isForward)
 {
-	if (!WAVE || (w->dbg & 2)) {
+	if (!WAVE || DSB_SEQ(w, 2)) {
 	uint32_t KEY_MASK = (1u << key_len) - 1;
 	uint32_t t_kmer_num = t_len - DSB_S_A_KMER_L + 1;
 	const uint32_t *heads = w->hh[hslot], *next = w->hn[hslot], *kk = w->hk[hslot];
@@ -1823,7 +1866,7 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 					uint32_t max_q = c_spd->q_pos + DSB_MAX_SMS_OVERLAP;
 					uint32_t max_t = c_spd->t_pos + DSB_MAX_SMS_OVERLAP;
 					int best = INT32_MIN;
-					const bool wv = WAVE && !(w->dbg & 4);
+					const bool wv = WAVE && !DSB_SEQ(w, 4);
 					for (int64_t pb = (int64_t)cs - 1; pb >= 0; pb -= (wv ? DSB_WV : 1)) {
 						int64_t ps = pb - (wv ? (int64_t)dsb_lane() : 0);
 						for (int64_t pe = (wv && ps >= 0) ? ps : 0; ps >= pe; ps--) { /* WAVE: one node per lane */
@@ -1948,7 +1991,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 		int max_score = (int)c_sms->len;
 		uint32_t max_pre_q = c_sms->q_pos + DSB_MAX_SMS_OVERLAP;
 		uint32_t max_pre_t = c_sms->t_pos + DSB_MAX_SMS_OVERLAP;
-		if (!WAVE || (w->dbg & 4)) {
+		if (!WAVE || DSB_SEQ(w, 4)) {
 			for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
 				dsb_spd_t *c_pre = dsb_sms(w, ps);
 				int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
@@ -2097,7 +2140,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 		int max_score = (int)c_sms->len;
 		uint32_t min_pre_q = c_sms->q_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
 		uint32_t min_pre_t = c_sms->t_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
-		if (!WAVE || (w->dbg & 4)) {
+		if (!WAVE || DSB_SEQ(w, 4)) {
 			for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
 				dsb_spd_t *c_pre = dsb_sms(w, ps);
 				if (c_pre->q_pos < min_pre_q) continue;

@@ -1,0 +1,163 @@
+/*
+ * dsb_kern.h — the phase kernels of classify part A (templates).  Each phase is compiled in
+ * its own translation unit (phase.hip, -DDSB_PH=n) so the phases build in parallel and get
+ * their own register allocation; kernels.hip launches them through dsb_phase_kernel_<n>().
+ */
+#ifndef DSB_KERN_H
+#define DSB_KERN_H
+#include <hip/hip_runtime.h>
+#include "dsb_ws.h"
+#include "dsb_gpu.h"
+
+/* minimum waves per SIMD requested from the register allocator (spills beyond) */
+/* measured on MI355X (C1 workload, fully inlined phase kernels): fast/slow seeding is fastest
+ * at 2 waves/SIMD, the scoring phase at 8, the lane-per-read phases at 2 */
+#ifndef DSB_MINW_LANE
+#define DSB_MINW_LANE 2
+#endif
+#ifndef DSB_MINW_FAST
+#define DSB_MINW_FAST 2
+#endif
+#ifndef DSB_MINW_DELA
+#define DSB_MINW_DELA 8
+#endif
+#ifndef DSB_MINW_RESOLVE
+#define DSB_MINW_RESOLVE 4
+#endif
+#define DSB_MINW_WAVE(PH) ((PH) == DSB_PH_DELA ? DSB_MINW_DELA : \
+			   ((PH) == DSB_PH_FAST0 || (PH) == DSB_PH_FAST1 || (PH) == DSB_PH_SLOW0 || (PH) == DSB_PH_SLOW1) \
+			   ? DSB_MINW_FAST : DSB_MINW_RESOLVE)
+#define DSB_WIN_LDS_BYTES ((DSB_WIN_BYTES + 15) & ~15)
+#define DSB_DELA_LDS (DSB_WIN_LDS_BYTES + DSB_SMS_LDS * sizeof(dsb_spd_t))
+static_assert(sizeof(dsb_rstate_t) <= DSB_STATE_BYTES, "per-read phase state must fit its workspace slot");
+
+/* One phase of classify part A (dsb_phase), one lane per read; the read's control state
+ * lives in its workspace between launches.  The last phase publishes the read's summary. */
+template <int PH, bool STATS>
+__global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+					       const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+					       uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+					       dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
+					       unsigned long long *__restrict__ gstats, uint32_t dbg)
+{
+	(void)dbg;
+	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= n)
+		return;
+	uint32_t r = order[t];
+	uint32_t L = len[r];
+	uint8_t *base = ws + ws_off[r];
+	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
+	dsb_read_ws w;
+	dsb_ws_init(&w, ix, base, L, cap);
+	dsb_rstate_t *sp = (dsb_rstate_t *)(base + dsb_layout(L, cap).state);
+	dsb_rflags_t f = {0, 0, 0, 0};
+	if (PH != DSB_PH_ISLAND)
+		dsb_state_load(&w, &f, sp);
+	uint64_t st[DSB_ST_N];
+	if (STATS) {
+		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
+		w.stats = st;
+	}
+	dsb_phase(&w, &f, PH);
+	dsb_state_save(&w, &f, sp);
+	if (PH == DSB_PH_DELA) {
+		dsb_read_out_t o;
+		o.n_hit = w.n_hit;
+		o.n_anchor = w.n_anc;
+		o.fast = w.fast_classify;
+		o.status = w.overflow;
+		o.reached_update = w.reached_update;
+		o.pad = 0;
+		o.hit_off = 0;
+		ro[r] = o;
+		if (w.overflow)
+			atomicAdd(n_overflow, 1u);
+	}
+	if (STATS)
+		for (int k = 0; k < DSB_ST_N; k++)
+			atomicAdd(gstats + 16 * PH + k, (unsigned long long)st[k]);
+}
+
+/* One phase of part A with one wavefront per read (dsb_wave.h), one wave per workgroup:
+ * fast seeding (FAST0/FAST1), chaining (RESOLVE_*), scoring (DELA).  The last phase
+ * publishes the read's summary like k_phase. */
+template <int PH, bool STATS>
+__global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+						    const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+						    uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+						    dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
+						    unsigned long long *__restrict__ gstats, uint32_t dbg)
+{
+	const int ph = PH;
+	uint32_t t = blockIdx.x;
+	if (t >= n)
+		return;
+	uint32_t lane = threadIdx.x;
+	uint32_t r = order[t];
+	uint32_t L = len[r];
+	uint8_t *base = ws + ws_off[r];
+	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
+	dsb_ws_layout lay = dsb_layout(L, cap);
+	dsb_read_ws w;
+	dsb_ws_init(&w, ix, base, L, cap);
+	dsb_rstate_t *sp = (dsb_rstate_t *)(base + lay.state);
+	dsb_rflags_t f;
+	dsb_state_load(&w, &f, sp);
+	w.dbg = dbg;
+	uint64_t st[DSB_ST_N];
+	if (STATS) {
+		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
+		w.stats = st;
+	}
+	if (PH == DSB_PH_DELA && (dbg & 512)) { /* scoring: reference windows and the sparse-DP prefix in LDS */
+		extern __shared__ uint8_t dsb_lds[];
+		w.win = dsb_lds;
+		w.sms_lds = (dsb_spd_t *)(dsb_lds + DSB_WIN_LDS_BYTES);
+	}
+	int active = dsb_phase_active(&w, &f, ph);
+	if (active) {
+		if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
+			uint64_t *hset = (uint64_t *)(base + lay.hset);
+			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
+				hset[k] = 0;
+			__syncthreads();
+			dsb_fast_classify_wave(&w, &w.sd[ph - DSB_PH_FAST0], hset);
+		} else if (ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) {
+			uint64_t *hset = (uint64_t *)(base + lay.hset);
+			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
+				hset[k] = 0;
+			__syncthreads();
+			dsb_slow_classify_wave(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem);
+		} else
+			dsb_phase<true>(&w, &f, ph);
+	}
+	__syncthreads();
+	if (lane == 0) {
+		if (active)
+			dsb_state_save(&w, &f, sp);
+		if (ph == DSB_PH_DELA) {
+			dsb_read_out_t o;
+			o.n_hit = w.n_hit;
+			o.n_anchor = w.n_anc;
+			o.fast = w.fast_classify;
+			o.status = w.overflow;
+			o.reached_update = w.reached_update;
+			o.pad = 0;
+			o.hit_off = 0;
+			ro[r] = o;
+			if (w.overflow)
+				atomicAdd(n_overflow, 1u);
+		}
+	}
+	if (STATS)
+		for (int k = 0; k < DSB_ST_N; k++)
+			if (st[k])
+				atomicAdd(gstats + 16 * PH + k, (unsigned long long)st[k]);
+}
+
+
+/* launch signature shared by the lane (k_phase) and wave (k_wave_phase) phase kernels */
+typedef void (*dsb_phase_fn)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
+			     const uint32_t *, uint32_t, dsb_read_out_t *, uint32_t *, unsigned long long *, uint32_t);
+#endif

@@ -26,24 +26,7 @@
 #include "dsb_ws.h"
 #include "dsb_gpu.h"
 
-/* minimum waves per SIMD requested from the register allocator (spills beyond) */
-/* measured on MI355X (C1 workload, fully inlined phase kernels): fast/slow seeding is fastest
- * at 2 waves/SIMD, the scoring phase at 8, the lane-per-read phases at 2 */
-#ifndef DSB_MINW_LANE
-#define DSB_MINW_LANE 2
-#endif
-#ifndef DSB_MINW_FAST
-#define DSB_MINW_FAST 2
-#endif
-#ifndef DSB_MINW_DELA
-#define DSB_MINW_DELA 8
-#endif
-#ifndef DSB_MINW_RESOLVE
-#define DSB_MINW_RESOLVE 4
-#endif
-#define DSB_MINW_WAVE(PH) ((PH) == DSB_PH_DELA ? DSB_MINW_DELA : \
-			   ((PH) == DSB_PH_FAST0 || (PH) == DSB_PH_FAST1 || (PH) == DSB_PH_SLOW0 || (PH) == DSB_PH_SLOW1) \
-			   ? DSB_MINW_FAST : DSB_MINW_RESOLVE)
+#include "dsb_kern.h"
 #include "dsb_debug.h"
 
 #define HIP_OK(x)                                                                                    \
@@ -120,134 +103,6 @@ __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ i
 	uint64_t bits = __ballot(e);
 	if (lane == 0)
 		ex[word] = bits;
-}
-
-#define DSB_WIN_LDS_BYTES ((DSB_WIN_BYTES + 15) & ~15)
-#define DSB_DELA_LDS (DSB_WIN_LDS_BYTES + DSB_SMS_LDS * sizeof(dsb_spd_t))
-static_assert(sizeof(dsb_rstate_t) <= DSB_STATE_BYTES, "per-read phase state must fit its workspace slot");
-
-/* One phase of classify part A (dsb_phase), one lane per read; the read's control state
- * lives in its workspace between launches.  The last phase publishes the read's summary. */
-template <int PH, bool STATS>
-__global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
-					       const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
-					       uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
-					       dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
-					       unsigned long long *__restrict__ gstats)
-{
-	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-	if (t >= n)
-		return;
-	uint32_t r = order[t];
-	uint32_t L = len[r];
-	uint8_t *base = ws + ws_off[r];
-	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
-	dsb_read_ws w;
-	dsb_ws_init(&w, ix, base, L, cap);
-	dsb_rstate_t *sp = (dsb_rstate_t *)(base + dsb_layout(L, cap).state);
-	dsb_rflags_t f = {0, 0, 0, 0};
-	if (PH != DSB_PH_ISLAND)
-		dsb_state_load(&w, &f, sp);
-	uint64_t st[DSB_ST_N];
-	if (STATS) {
-		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
-		w.stats = st;
-	}
-	dsb_phase(&w, &f, PH);
-	dsb_state_save(&w, &f, sp);
-	if (PH == DSB_PH_DELA) {
-		dsb_read_out_t o;
-		o.n_hit = w.n_hit;
-		o.n_anchor = w.n_anc;
-		o.fast = w.fast_classify;
-		o.status = w.overflow;
-		o.reached_update = w.reached_update;
-		o.pad = 0;
-		o.hit_off = 0;
-		ro[r] = o;
-		if (w.overflow)
-			atomicAdd(n_overflow, 1u);
-	}
-	if (STATS)
-		for (int k = 0; k < DSB_ST_N; k++)
-			atomicAdd(gstats + 16 * PH + k, (unsigned long long)st[k]);
-}
-
-/* One phase of part A with one wavefront per read (dsb_wave.h), one wave per workgroup:
- * fast seeding (FAST0/FAST1), chaining (RESOLVE_*), scoring (DELA).  The last phase
- * publishes the read's summary like k_phase. */
-template <int PH, bool STATS>
-__global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
-						    const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
-						    uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
-						    dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
-						    unsigned long long *__restrict__ gstats, uint32_t dbg)
-{
-	const int ph = PH;
-	uint32_t t = blockIdx.x;
-	if (t >= n)
-		return;
-	uint32_t lane = threadIdx.x;
-	uint32_t r = order[t];
-	uint32_t L = len[r];
-	uint8_t *base = ws + ws_off[r];
-	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
-	dsb_ws_layout lay = dsb_layout(L, cap);
-	dsb_read_ws w;
-	dsb_ws_init(&w, ix, base, L, cap);
-	dsb_rstate_t *sp = (dsb_rstate_t *)(base + lay.state);
-	dsb_rflags_t f;
-	dsb_state_load(&w, &f, sp);
-	w.dbg = dbg;
-	uint64_t st[DSB_ST_N];
-	if (STATS) {
-		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
-		w.stats = st;
-	}
-	if (PH == DSB_PH_DELA && (dbg & 512)) { /* scoring: reference windows and the sparse-DP prefix in LDS */
-		extern __shared__ uint8_t dsb_lds[];
-		w.win = dsb_lds;
-		w.sms_lds = (dsb_spd_t *)(dsb_lds + DSB_WIN_LDS_BYTES);
-	}
-	int active = dsb_phase_active(&w, &f, ph);
-	if (active) {
-		if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
-			uint64_t *hset = (uint64_t *)(base + lay.hset);
-			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
-				hset[k] = 0;
-			__syncthreads();
-			dsb_fast_classify_wave(&w, &w.sd[ph - DSB_PH_FAST0], hset);
-		} else if (ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) {
-			uint64_t *hset = (uint64_t *)(base + lay.hset);
-			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
-				hset[k] = 0;
-			__syncthreads();
-			dsb_slow_classify_wave(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem);
-		} else
-			dsb_phase<true>(&w, &f, ph);
-	}
-	__syncthreads();
-	if (lane == 0) {
-		if (active)
-			dsb_state_save(&w, &f, sp);
-		if (ph == DSB_PH_DELA) {
-			dsb_read_out_t o;
-			o.n_hit = w.n_hit;
-			o.n_anchor = w.n_anc;
-			o.fast = w.fast_classify;
-			o.status = w.overflow;
-			o.reached_update = w.reached_update;
-			o.pad = 0;
-			o.hit_off = 0;
-			ro[r] = o;
-			if (w.overflow)
-				atomicAdd(n_overflow, 1u);
-		}
-	}
-	if (STATS)
-		for (int k = 0; k < DSB_ST_N; k++)
-			if (st[k])
-				atomicAdd(gstats + 16 * PH + k, (unsigned long long)st[k]);
 }
 
 template <bool STATS>
@@ -484,49 +339,25 @@ static double now_ms(void)
 	return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
 }
 
-typedef void (*phase_kernel_t)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
-			       const uint32_t *, uint32_t, dsb_read_out_t *, uint32_t *, unsigned long long *);
-template <int PH>
-static phase_kernel_t phase_kernel(bool stats)
-{
-	return stats ? k_phase<PH, true> : k_phase<PH, false>;
-}
-static phase_kernel_t phase_kernel_at(int ph, bool stats)
-{
-	switch (ph) {
-	case 0: return phase_kernel<0>(stats);
-	case 1: return phase_kernel<1>(stats);
-	case 2: return phase_kernel<2>(stats);
-	case 3: return phase_kernel<3>(stats);
-	case 4: return phase_kernel<4>(stats);
-	case 5: return phase_kernel<5>(stats);
-	case 6: return phase_kernel<6>(stats);
-	case 7: return phase_kernel<7>(stats);
-	default: return phase_kernel<8>(stats);
-	}
+/* the phase kernels live in their own translation units (phase.hip, one per phase) */
+extern "C" {
+dsb_phase_fn dsb_phase_kernel_0(int wave, int stats);
+dsb_phase_fn dsb_phase_kernel_1(int wave, int stats);
+dsb_phase_fn dsb_phase_kernel_2(int wave, int stats);
+dsb_phase_fn dsb_phase_kernel_3(int wave, int stats);
+dsb_phase_fn dsb_phase_kernel_4(int wave, int stats);
+dsb_phase_fn dsb_phase_kernel_5(int wave, int stats);
+dsb_phase_fn dsb_phase_kernel_6(int wave, int stats);
+dsb_phase_fn dsb_phase_kernel_7(int wave, int stats);
+dsb_phase_fn dsb_phase_kernel_8(int wave, int stats);
 }
 static_assert(DSB_PH_N == 9, "phase dispatch table");
-
-typedef void (*wave_kernel_t)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
-			      const uint32_t *, uint32_t, dsb_read_out_t *, uint32_t *, unsigned long long *, uint32_t);
-template <int PH>
-static wave_kernel_t wave_kernel(bool stats)
+static dsb_phase_fn phase_kernel_at(int ph, int wave, bool stats)
 {
-	return stats ? k_wave_phase<PH, true> : k_wave_phase<PH, false>;
-}
-static wave_kernel_t wave_kernel_at(int ph, bool stats)
-{
-	switch (ph) {
-	case DSB_PH_FAST0: return wave_kernel<DSB_PH_FAST0>(stats);
-	case DSB_PH_FAST1: return wave_kernel<DSB_PH_FAST1>(stats);
-	case DSB_PH_RESOLVE_F: return wave_kernel<DSB_PH_RESOLVE_F>(stats);
-	case DSB_PH_SLOW0: return wave_kernel<DSB_PH_SLOW0>(stats);
-	case DSB_PH_SLOW1: return wave_kernel<DSB_PH_SLOW1>(stats);
-	case DSB_PH_RESOLVE_S0: return wave_kernel<DSB_PH_RESOLVE_S0>(stats);
-	case DSB_PH_RESOLVE_S1: return wave_kernel<DSB_PH_RESOLVE_S1>(stats);
-	case DSB_PH_DELA: return wave_kernel<DSB_PH_DELA>(stats);
-	default: return nullptr;
-	}
+	static dsb_phase_fn (*const get[DSB_PH_N])(int, int) = {
+		dsb_phase_kernel_0, dsb_phase_kernel_1, dsb_phase_kernel_2, dsb_phase_kernel_3, dsb_phase_kernel_4,
+		dsb_phase_kernel_5, dsb_phase_kernel_6, dsb_phase_kernel_7, dsb_phase_kernel_8};
+	return get[ph](wave, stats ? 1 : 0);
 }
 
 static float ev_ms(dsb_gpu_dev *g)
@@ -599,15 +430,21 @@ static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl,
 			 uint32_t m)
 {
 	hipStream_t s = g->stream;
-	if ((wave_phases() >> ph) & 1)
-		hipLaunchKernelGGL(wave_kernel_at(ph, stats), dim3(m), dim3(64),
-				   (ph == DSB_PH_DELA && (wave_dbg() & 512)) ? DSB_DELA_LDS : 0, s, g->d, cl,
+	int wave = (int)((wave_phases() >> ph) & 1);
+	dsb_phase_fn fn = phase_kernel_at(ph, wave, stats);
+	if (!fn) { /* a lane-per-read phase variant that is not compiled in (build with DSB_LANE_PHASES=1) */
+		fprintf(stderr, "[dsb] phase %d: no %s-per-read kernel in this build\n", ph, wave ? "wave" : "lane");
+		abort();
+	}
+	uint32_t dbg = wave_dbg();
+	if (wave)
+		hipLaunchKernelGGL(fn, dim3(m), dim3(64), (ph == DSB_PH_DELA && (dbg & 512)) ? DSB_DELA_LDS : 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
-				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), wave_dbg());
+				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), dbg);
 	else
-		hipLaunchKernelGGL(phase_kernel_at(ph, stats), dim3((m + 63) / 64), dim3(64), 0, s, g->d, cl,
-				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
-				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>());
+		hipLaunchKernelGGL(fn, dim3((m + 63) / 64), dim3(64), 0, s, g->d, cl, g->ws_off.as<uint64_t>(),
+				   g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(), g->cnt.as<uint32_t>(),
+				   g->stats.as<unsigned long long>(), dbg);
 }
 
 /* a batch of reads resident in HBM (sequences only) + its results */

@@ -1,0 +1,36 @@
+/*
+ * phase.hip — one phase kernel of classify part A per translation unit: compiled once per
+ * phase with -DDSB_PH=<n> (desamba-so_amd/Makefile), so the nine phases build in parallel
+ * and each gets its own register allocation.  kernels.hip obtains the kernel through
+ * dsb_phase_kernel_<n>(wave, stats).
+ *
+ * Phase 0 (island scan) runs one lane per read; phases 1-8 run one wavefront per read.  The
+ * lane-per-read variants of phases 1-8 are diagnostics only (DSB_WAVE_PHASES) and are
+ * compiled in with -DDSB_LANE_PHASES=1.
+ */
+#include "dsb_kern.h"
+
+#ifndef DSB_PH
+#error "compile with -DDSB_PH=<phase number>"
+#endif
+#ifndef DSB_LANE_PHASES
+#define DSB_LANE_PHASES 0
+#endif
+#define DSB_CAT_(a, b) a##b
+#define DSB_CAT(a, b) DSB_CAT_(a, b)
+
+extern "C" dsb_phase_fn DSB_CAT(dsb_phase_kernel_, DSB_PH)(int wave, int stats)
+{
+#if DSB_PH == 0
+	(void)wave;
+	return stats ? k_phase<0, true> : k_phase<0, false>;
+#else
+	if (wave)
+		return stats ? k_wave_phase<DSB_PH, true> : k_wave_phase<DSB_PH, false>;
+#if DSB_LANE_PHASES
+	return stats ? k_phase<DSB_PH, true> : k_phase<DSB_PH, false>;
+#else
+	return nullptr;
+#endif
+#endif
+}
