@@ -30,14 +30,23 @@ typedef struct { uint32_t ref_list, length; } dsb_unitig_t;
 #define DSB_LV_DIM 20
 #define DSB_MIN_UNI_L 35
 #define DSB_MIN_READ_LEN 40
+#define DSB_MAX_DOLLAR 4     /* '$' symbols in the BWT the HBM occ layout supports (one in practice) */
+#define DSB_OCC_LINE_U64 16  /* u64 words per 256-symbol occ line */
 
 /*
  * Device-visible index: raw pointers into HBM (or host memory for the
  * kernel-logic CPU emulation used only by tests).
  */
 typedef struct {
-	const uint8_t *bwt_occ;      /* 168-B blocks per 256 BWT symbols (bwt.c:32-42) */
-	uint64_t byteLen;
+	/* occ/rank table re-laid out for HBM: one 128-B line per 256 BWT symbols,
+	 * u64 cnt[4] (occ of A,C,G,T at the line start) | u64 sym[8] (2-bit symbols, 32 per word,
+	 * '#'/'$' stored as 0) | u64 spc[4] (1 = '#' or '$', 64 per word).  Replaces the
+	 * reference's 168-B blocks (bwt.c:32-42) losslessly: '$' rows are listed below and the
+	 * '#' count is line start - A - C - G - T - '$' before it. */
+	const uint64_t *occ;
+	uint64_t n_occ_line;
+	uint64_t dollar_row[DSB_MAX_DOLLAR];
+	int n_dollar;
 	uint64_t rank[6];            /* rank[5] = rank[0]-1 (bwt.c:81) */
 	const uint64_t *hash_index;  /* (2^26+1) u64, 13-mer prefix -> SA interval (bwt.c:83-85) */
 	const dsb_sa_t *sa;

@@ -121,29 +121,93 @@ DSB_HD uint32_t dsb_nib_eq(uint64_t x, uint32_t c, uint32_t n)
 	return n - (uint32_t)__builtin_popcountll(nz & m);
 }
 
+/* Number of 2-bit fields equal to c (pat = c in every field) among the low n (<= 32) fields. */
+DSB_HD uint32_t dsb_sym2_eq(uint64_t x, uint64_t pat, int n)
+{
+	uint64_t y = x ^ pat;
+	uint64_t z = ~(y | (y >> 1)) & 0x5555555555555555ull;
+	uint64_t m = (n >= 32) ? ~0ull : (n <= 0 ? 0ull : ((1ull << (2 * n)) - 1));
+	return (uint32_t)__builtin_popcountll(z & m);
+}
+DSB_HD uint64_t dsb_low_mask(int n) /* low n (0..64) bits */
+{
+	return (n >= 64) ? ~0ull : (n <= 0 ? 0ull : ((1ull << n) - 1));
+}
+
 /*
- * occ, src/bwt.c:43-65: checkpoint count of c at the 256-symbol block + number of c in
- * [block start, r).  c == 0xff: c := symbol at r, and symbol 5 ('$') returns DOLLOR_POS.
- * The reference counts 4 nibbles per AGCTCounter lookup; here 16 per popcount.
+ * occ, src/bwt.c:43-65: number of c in BWT[0, r) — the line's checkpoint + the matching
+ * symbols before r in the line.  c == 0xff: c := symbol at r, and '$' (5) returns DOLLOR_POS.
+ * One 128-B line per 256 symbols (dsb_types.h): the whole line is fetched with independent
+ * loads (one memory round trip), the symbol at r and the counts are computed from registers.
  */
 DSB_HD uint64_t dsb_occ(const dsb_dindex_t *ix, uint64_t r, uint8_t *c)
 {
-	const uint8_t *blk = ix->bwt_occ + (r >> 8) * 168;
-	const uint64_t *w = (const uint64_t *)(blk + 40);
-	uint32_t within = (uint32_t)(r & 0xff);
+	const uint64_t *ln = (const uint64_t *)__builtin_assume_aligned(ix->occ + (r >> 8) * DSB_OCC_LINE_U64, 128);
+	uint64_t v[DSB_OCC_LINE_U64];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+	for (int k = 0; k < DSB_OCC_LINE_U64; k++)
+		v[k] = ln[k];
+	int within = (int)(r & 0xff);
 	if (*c == 0xff) {
-		uint64_t word = w[within >> 4];
-		*c = (uint8_t)((word >> ((within & 15) << 2)) & 0xf);
-		if (*c == 5)
-			return ix->dollor_pos;
+		int wi = within >> 5, si = within >> 6;
+		uint64_t sw = v[4], pw = v[12];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+		for (int k = 1; k < 8; k++)
+			sw = (wi == k) ? v[4 + k] : sw;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+		for (int k = 1; k < 4; k++)
+			pw = (si == k) ? v[12 + k] : pw;
+		if ((pw >> (within & 63)) & 1) {
+			*c = 4;
+			for (int d = 0; d < ix->n_dollar; d++)
+				if (ix->dollar_row[d] == r)
+					*c = 5;
+			if (*c == 5)
+				return ix->dollor_pos;
+		} else
+			*c = (uint8_t)((sw >> (2 * (within & 31))) & 3);
 	}
-	uint64_t base = ((const uint64_t *)blk)[*c];
-	uint32_t cc = *c, cnt = 0, full = within >> 4;
-	for (uint32_t k = 0; k < full; k++)
-		cnt += dsb_nib_eq(w[k], cc, 16);
-	if (within & 15)
-		cnt += dsb_nib_eq(w[full], cc, within & 15);
-	return base + cnt;
+	uint32_t cc = *c;
+	uint64_t pat = 0x5555555555555555ull * (cc & 3);
+	uint64_t base = v[0];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+	for (int k = 1; k < 4; k++)
+		base = (cc == (uint32_t)k) ? v[k] : base;
+	uint32_t spc = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+	for (int k = 0; k < 4; k++)
+		spc += (uint32_t)__builtin_popcountll(v[12 + k] & dsb_low_mask(within - 64 * k));
+	if (cc < 4) {
+		uint32_t cnt = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+		for (int k = 0; k < 8; k++)
+			cnt += dsb_sym2_eq(v[4 + k], pat, within - 32 * k);
+		if (cc == 0) /* '#' and '$' are stored as 0 */
+			cnt -= spc;
+		return base + cnt;
+	}
+	/* '#': line start - A - C - G - T - '$' before the line, then the specials before r that are not '$' */
+	uint64_t start = r & ~255ull;
+	uint64_t h = start - v[0] - v[1] - v[2] - v[3];
+	for (int d = 0; d < ix->n_dollar; d++) {
+		if (ix->dollar_row[d] < start)
+			h--;
+		else if (ix->dollar_row[d] < r)
+			spc--;
+	}
+	return h + spc;
 }
 
 /* LF step with unknown c: returns new row and the symbol (src/cly.c:744, 782, 1361) */

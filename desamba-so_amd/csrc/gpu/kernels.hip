@@ -276,9 +276,11 @@ extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
 	HIP_OK(hipEventCreate(&g->ev_b));
 	dsb_dindex_t &h = g->h;
 	memset(&h, 0, sizeof(h));
-	/* bwt_occ: + 256 B slack (occ reads whole 16-nibble words) */
-	if (upload(g, ix->bwt_occ, ix->byteLen + 256, &h.bwt_occ, err, errn)) return -1;
-	h.byteLen = ix->byteLen;
+	/* occ lines (128 B per 256 BWT symbols, re-laid out by the loader) + one zero line */
+	if (upload(g, ix->occ, (ix->n_occ_line + 1) * DSB_OCC_LINE_U64, &h.occ, err, errn)) return -1;
+	h.n_occ_line = ix->n_occ_line;
+	memcpy(h.dollar_row, ix->dollar_row, sizeof(h.dollar_row));
+	h.n_dollar = ix->n_dollar;
 	memcpy(h.rank, ix->rank, sizeof(h.rank));
 	if (upload(g, ix->hash_index, (1ull << 26) + 1, &h.hash_index, err, errn)) return -1;
 	if (upload(g, ix->sa, ix->sa_size, &h.sa, err, errn)) return -1;

@@ -75,6 +75,59 @@ static void set_ekmer_par(dsb_index *ix)
 	ix->single_base_max = (int)(0.8 * l); /* SINGLE_BASE_MAX_RATIO_THEADHOLD * len_e_kmer */
 }
 
+/*
+ * occ table re-layout: the reference's 168-B blocks (bwt.c:32-42: u64 count of
+ * A,C,G,T,'#' before the block + 256 4-bit symbols) -> one 128-B line per 256 symbols.  The
+ * '#' checkpoints the new line drops are re-derived and checked against the file for every
+ * block, so the re-layout is verified lossless on each index it loads.
+ */
+static int occ_relayout(dsb_index *ix, char *err, size_t errn)
+{
+	if (ix->byteLen % 168) {
+		snprintf(err, errn, "deSAMBA.bwt: occ section of %lu bytes is not a whole number of 168-B blocks",
+			 (unsigned long)ix->byteLen);
+		return -1;
+	}
+	uint64_t nb = ix->byteLen / 168;
+	ix->n_occ_line = nb;
+	ix->occ = xm((nb + 1) * DSB_OCC_LINE_U64 * 8); /* + one zero line past the end */
+	memset(ix->occ, 0, (nb + 1) * DSB_OCC_LINE_U64 * 8);
+	ix->n_dollar = 0;
+	uint64_t dollars = 0;
+	for (uint64_t b = 0; b < nb; b++) {
+		const uint8_t *src = ix->bwt_occ + b * 168;
+		uint64_t cnt[5];
+		memcpy(cnt, src, 40);
+		uint64_t *ln = ix->occ + b * DSB_OCC_LINE_U64;
+		uint64_t hash_before = (b << 8) - cnt[0] - cnt[1] - cnt[2] - cnt[3] - dollars;
+		if (hash_before != cnt[4]) {
+			snprintf(err, errn, "deSAMBA.bwt: block %lu: '#' checkpoint %lu != %lu derived (unexpected occ layout)",
+				 (unsigned long)b, (unsigned long)cnt[4], (unsigned long)hash_before);
+			return -1;
+		}
+		memcpy(ln, cnt, 32);
+		for (uint32_t k = 0; k < 256; k++) {
+			uint64_t w;
+			memcpy(&w, src + 40 + 8 * (k >> 4), 8);
+			uint32_t nib = (uint32_t)((w >> ((k & 15) << 2)) & 0xf);
+			if (nib < 4) {
+				ln[4 + (k >> 5)] |= (uint64_t)nib << (2 * (k & 31));
+			} else {
+				ln[12 + (k >> 6)] |= 1ull << (k & 63);
+				if (nib == 5) {
+					if (ix->n_dollar >= DSB_MAX_DOLLAR) {
+						snprintf(err, errn, "deSAMBA.bwt: more than %d '$' symbols (unsupported)", DSB_MAX_DOLLAR);
+						return -1;
+					}
+					ix->dollar_row[ix->n_dollar++] = (b << 8) + k;
+					dollars++;
+				}
+			}
+		}
+	}
+	return 0;
+}
+
 int dsb_index_load_files(dsb_index *ix, const char *dir, char *err, size_t errn)
 {
 	FILE *f;
@@ -86,6 +139,9 @@ int dsb_index_load_files(dsb_index *ix, const char *dir, char *err, size_t errn)
 	if (rd(f, ix->bwt_occ, 1, ix->byteLen, "bwt occ", err, errn)) goto fail;
 	if (rd(f, ix->rank, 8, 5, "rank", err, errn)) goto fail;
 	ix->rank[5] = ix->rank[0] - 1;
+	if (occ_relayout(ix, err, errn)) goto fail;
+	free(ix->bwt_occ);
+	ix->bwt_occ = NULL;
 	{
 		uint64_t n = (1ull << (DSB_L_PRE_IDX << 1)) + 1;
 		ix->hash_index = xm(n * 8);
@@ -255,6 +311,7 @@ int dsb_taxonomy_load(dsb_index *ix, const char *dir, char *err, size_t errn)
 void dsb_index_free_host_tables(dsb_index *ix)
 {
 	free(ix->bwt_occ); ix->bwt_occ = NULL;
+	free(ix->occ); ix->occ = NULL;
 	free(ix->hash_index); ix->hash_index = NULL;
 	free(ix->sa); ix->sa = NULL;
 	free(ix->ek0); ix->ek0 = NULL;
@@ -267,7 +324,8 @@ void dsb_index_free_host_tables(dsb_index *ix)
 void dsb_index_host_view(const dsb_index *ix, dsb_dindex_t *d)
 {
 	memset(d, 0, sizeof(*d));
-	d->bwt_occ = ix->bwt_occ; d->byteLen = ix->byteLen;
+	d->occ = ix->occ; d->n_occ_line = ix->n_occ_line;
+	memcpy(d->dollar_row, ix->dollar_row, sizeof(d->dollar_row)); d->n_dollar = ix->n_dollar;
 	memcpy(d->rank, ix->rank, sizeof(d->rank));
 	d->hash_index = ix->hash_index;
 	d->sa = ix->sa; d->sa_size = ix->sa_size; d->dollor_pos = ix->dollor_pos;
