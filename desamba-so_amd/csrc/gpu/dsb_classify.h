@@ -126,6 +126,13 @@ enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, 
        DSB_ST_T_MEM,    /* shader clocks inside bwt_MEM_search (stats kernels only) */
        DSB_ST_T_MAP,    /* shader clocks inside map_seed (stats kernels only) */
        DSB_ST_N };
+/* scoring phase timers (stats kernels, lane 0): slots unused by that phase */
+#define DSB_ST_T_BUILD DSB_ST_T_MEM   /* build_hash_table_M2 */
+#define DSB_ST_T_MATCH DSB_ST_T_MAP   /* sdp_match */
+#define DSB_ST_T_WIN DSB_ST_EK1       /* reference windows: get_ref + pattern fill */
+#define DSB_ST_T_ALL DSB_ST_EK2       /* the whole of delete_small_score_rst part A */
+#define DSB_T0() ((w->stats && dsb_lane() == 0) ? dsb_clock() : 0)
+#define DSB_T1(slot, t0) do { if (w->stats && dsb_lane() == 0) w->stats[slot] += dsb_clock() - (t0); } while (0)
 
 DSB_HD uint64_t dsb_clock(void)
 {
@@ -1396,6 +1403,7 @@ DSB_HDN void dsb_resolve_tree(dsb_read_ws *w)
 template <bool WAVE>
 DSB_HD void dsb_get_ref_win(dsb_read_ws *w, uint8_t *ref_str, uint64_t uni_offset, uint32_t length)
 {
+	uint64_t tw0 = DSB_T0();
 	if (!WAVE || DSB_SEQ(w, 8)) {
 		dsb_get_ref_w(w, ref_str, uni_offset, length, 1);
 	} else {
@@ -1412,6 +1420,7 @@ DSB_HD void dsb_get_ref_win(dsb_read_ws *w, uint8_t *ref_str, uint64_t uni_offse
 		}
 		dsb_wsync();
 	}
+	DSB_T1(DSB_ST_T_WIN, tw0);
 }
 
 /* fill ref[lo, hi) with the stack pattern */
@@ -1605,7 +1614,7 @@ DSB_HD int dsb_MEM_search(const uint8_t *q, const uint8_t *t, int forward, int m
  * WAVE: every 4th window position (the only ones looked up) is one lane; a lane's matches
  * keep the hash-list order, lanes keep position order (prefix-sum compaction). */
 template <bool WAVE>
-DSB_HDN void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const uint8_t *q_str, const uint8_t *t_str,
+DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const uint8_t *q_str, const uint8_t *t_str,
 			    uint32_t t_len, int key_len, int hslot, uint32_t t_st, int isForward)
 {
 	if (!WAVE || DSB_SEQ(w, 2)) {
@@ -1813,6 +1822,15 @@ DSB_HDN void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const u
 		}
 		dsb_wsync();
 	}
+}
+
+template <bool WAVE>
+DSB_HD void dsb_sdp_match(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, const uint8_t *q_str, const uint8_t *t_str,
+			  uint32_t t_len, int key_len, int hslot, uint32_t t_st, int isForward)
+{
+	uint64_t t0 = DSB_T0();
+	dsb_sdp_match_impl<WAVE>(w, q_bg, q_ed, q_str, t_str, t_len, key_len, hslot, t_st, isForward);
+	DSB_T1(DSB_ST_T_MATCH, t0);
 }
 
 /* sdp_middle_M2, src/cly.c:2439-2525 */
@@ -2230,7 +2248,9 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 template <bool WAVE>
 DSB_HDN void dsb_get_score(dsb_read_ws *w, uint32_t l_read)
 {
+	uint64_t tb0 = DSB_T0();
 	int key_len = dsb_build_hash_table<WAVE>(w, (int)l_read);
+	DSB_T1(DSB_ST_T_BUILD, tb0);
 	for (uint32_t i = 0; i < w->n_hit; i++) {
 		if (w->hit[i].sum_score == 0)
 			continue;
@@ -2286,7 +2306,9 @@ DSB_HDN void dsb_delete_small_A(dsb_read_ws *w)
 	w->n_hit = DSB_MIN(400u, w->n_hit);
 	uint32_t l_read = w->L;
 	dsb_sc_hash_idx(w);
+	uint64_t ta0 = DSB_T0();
 	dsb_get_score<WAVE>(w, l_read);
+	DSB_T1(DSB_ST_T_ALL, ta0);
 	if (w->overflow)
 		return;
 	uint32_t n = w->n_hit;

@@ -16,26 +16,40 @@
 #include "dsb_core.h"
 
 #if defined(__HIP_DEVICE_COMPILE__)
+/*
+ * Reductions and scans use DPP row operations (16-lane rows, VALU latency) plus v_readlane
+ * for the four row totals, instead of ds_bpermute shuffles (an LDS round trip per step).
+ * All helpers assume the whole wave is active (they are called from wave-uniform code).
+ */
 #define DSB_WV 64
+#define DSB_DPP_ROW_SHR(n) (0x110 + (n))
+#define DSB_DPP_ROW_ROR(n) (0x120 + (n))
 DSB_HD uint32_t dsb_lane(void) { return __lane_id(); }
 DSB_HD void dsb_wsync(void) { __syncthreads(); }
+DSB_HD int dsb_rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+/* max over the wave, returned uniform */
 DSB_HD int dsb_wmax(int v)
 {
-	for (int o = 32; o; o >>= 1)
-		v = max(v, __shfl_xor(v, o));
-	return v;
+	v = max(v, __builtin_amdgcn_update_dpp(v, v, DSB_DPP_ROW_ROR(1), 0xf, 0xf, false));
+	v = max(v, __builtin_amdgcn_update_dpp(v, v, DSB_DPP_ROW_ROR(2), 0xf, 0xf, false));
+	v = max(v, __builtin_amdgcn_update_dpp(v, v, DSB_DPP_ROW_ROR(4), 0xf, 0xf, false));
+	v = max(v, __builtin_amdgcn_update_dpp(v, v, DSB_DPP_ROW_ROR(8), 0xf, 0xf, false));
+	return max(max(dsb_rdlane(v, 0), dsb_rdlane(v, 16)), max(dsb_rdlane(v, 32), dsb_rdlane(v, 48)));
 }
 /* exclusive prefix sum over the wave; *tot = sum over all lanes */
 DSB_HD uint32_t dsb_wscan(uint32_t v, uint32_t *tot)
 {
-	uint32_t lane = __lane_id(), x = v;
-	for (int o = 1; o < 64; o <<= 1) {
-		uint32_t y = __shfl_up(x, o);
-		if (lane >= (uint32_t)o)
-			x += y;
-	}
-	*tot = __shfl(x, 63);
-	return x - v;
+	int x = (int)v;
+	x += __builtin_amdgcn_update_dpp(0, x, DSB_DPP_ROW_SHR(1), 0xf, 0xf, true);
+	x += __builtin_amdgcn_update_dpp(0, x, DSB_DPP_ROW_SHR(2), 0xf, 0xf, true);
+	x += __builtin_amdgcn_update_dpp(0, x, DSB_DPP_ROW_SHR(4), 0xf, 0xf, true);
+	x += __builtin_amdgcn_update_dpp(0, x, DSB_DPP_ROW_SHR(8), 0xf, 0xf, true);
+	uint32_t r0 = (uint32_t)dsb_rdlane(x, 15), r1 = (uint32_t)dsb_rdlane(x, 31), r2 = (uint32_t)dsb_rdlane(x, 47),
+		 r3 = (uint32_t)dsb_rdlane(x, 63);
+	uint32_t row = __lane_id() >> 4;
+	uint32_t add = (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
+	*tot = r0 + r1 + r2 + r3;
+	return (uint32_t)x + add - v;
 }
 DSB_HD uint64_t dsb_wmax64(uint64_t v)
 {
@@ -47,7 +61,8 @@ DSB_HD uint64_t dsb_wmax64(uint64_t v)
 	return v;
 }
 DSB_HD uint64_t dsb_wballot(int p) { return __ballot(p); }
-DSB_HD int dsb_wshfl(int v, int src) { return __shfl(v, src); }
+/* value of lane `src`; src must be wave-uniform (v_readlane) */
+DSB_HD int dsb_wshfl(int v, int src) { return dsb_rdlane(v, src); }
 #else
 #define DSB_WV 1
 DSB_HD uint32_t dsb_lane(void) { return 0; }
