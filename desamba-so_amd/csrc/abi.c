@@ -23,6 +23,7 @@
 #include "gpu/dsb_gpu.h"
 #include "../../include/desamba.h"
 #include "../../include/desamba_mi355x.h"
+_Static_assert(sizeof(((dsb_timing_t *)0)->stats) == sizeof(((dsb_gpu_timing *)0)->stats), "ABI timing.stats mirrors dsb_gpu_timing.stats");
 
 struct dsb_thread_state {
 	int thread_id;
@@ -124,7 +125,7 @@ int dsb_classify_text(void *idx, const char *text, uint64_t text_n, int format, 
 		timing->n_retry = gt.n_retry;
 		timing->n_chunks = gt.n_chunks;
 		timing->seed_positions = gt.seed_positions;
-		for (int k = 0; k < 160; k++) timing->stats[k] = gt.stats[k];
+		for (int k = 0; k < DSB_N_STATS; k++) timing->stats[k] = gt.stats[k];
 	}
 	free(ro);
 	free(hits);
@@ -198,7 +199,7 @@ static void copy_timing(dsb_timing_t *t, const dsb_gpu_timing *gt)
 	t->n_retry = gt->n_retry;
 	t->n_chunks = gt->n_chunks;
 	t->seed_positions = gt->seed_positions;
-	for (int k = 0; k < 160; k++) t->stats[k] = gt->stats[k];
+	for (int k = 0; k < DSB_N_STATS; k++) t->stats[k] = gt->stats[k];
 }
 
 dsb_batch *dsb_batch_create(void *idx, const char *text, uint64_t text_n, dsb_timing_t *timing)

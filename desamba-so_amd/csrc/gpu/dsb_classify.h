@@ -102,7 +102,7 @@ typedef struct {
 	dsb_chain_t *hit_tmp;
 	dsb_spd_t *sms; uint32_t n_sms;
 	dsb_spd_t *sms_lds;     /* wave scoring: the first DSB_SMS_LDS sms entries live in LDS */
-	uint32_t *hh[2], *ht[2], *hn[2], *hk[2]; /* read 9-mer hash: heads, tails, next, kmer */
+	uint32_t *hh[2], *hn[2]; /* read 9-mer hash per strand: list heads per key, one node per position */
 	dsb_sch_t *sch;         /* 256 + 2*400 */
 	uint8_t *win;           /* DSB_WIN_BYTES: sdp_middle ref[2000] and sdp_right/left ref[1000] windows */
 	dsb_mem_t *mem;         /* 16 MEM results per lane (slow mode) */
@@ -125,12 +125,15 @@ enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, 
        DSB_ST_NODE,     /* hash-list nodes visited by those lookups (8 B each) */
        DSB_ST_T_MEM,    /* shader clocks inside bwt_MEM_search (stats kernels only) */
        DSB_ST_T_MAP,    /* shader clocks inside map_seed (stats kernels only) */
+       /* scoring phase clocks (stats kernels, lane 0) */
+       DSB_ST_T_BUILD,  /* build_hash_table_M2 */
+       DSB_ST_T_MATCH,  /* sdp_match */
+       DSB_ST_T_WIN,    /* reference windows: get_ref */
+       DSB_ST_T_ALL,    /* get_score_M2 as a whole */
+       DSB_ST_T_DPM,    /* sdp_middle predecessor scans */
+       DSB_ST_T_DPS,    /* sdp_right / sdp_left predecessor scans */
+       DSB_ST_T_FILL,   /* stack-pattern fills of the windows */
        DSB_ST_N };
-/* scoring phase timers (stats kernels, lane 0): slots unused by that phase */
-#define DSB_ST_T_BUILD DSB_ST_T_MEM   /* build_hash_table_M2 */
-#define DSB_ST_T_MATCH DSB_ST_T_MAP   /* sdp_match */
-#define DSB_ST_T_WIN DSB_ST_EK1       /* reference windows: get_ref + pattern fill */
-#define DSB_ST_T_ALL DSB_ST_EK2       /* the whole of delete_small_score_rst part A */
 #define DSB_T0() ((w->stats && dsb_lane() == 0) ? dsb_clock() : 0)
 #define DSB_T1(slot, t0) do { if (w->stats && dsb_lane() == 0) w->stats[slot] += dsb_clock() - (t0); } while (0)
 
@@ -1425,7 +1428,7 @@ DSB_HD void dsb_get_ref_win(dsb_read_ws *w, uint8_t *ref_str, uint64_t uni_offse
 
 /* fill ref[lo, hi) with the stack pattern */
 template <bool WAVE>
-DSB_HD void dsb_fill_pattern(uint8_t *ref, int lo, int hi)
+DSB_HD void dsb_fill_pattern_impl(uint8_t *ref, int lo, int hi)
 {
 	if constexpr (!WAVE) {
 		for (int k = lo; k < hi; k++) ref[k] = DSB_STACK_PATTERN;
@@ -1433,6 +1436,13 @@ DSB_HD void dsb_fill_pattern(uint8_t *ref, int lo, int hi)
 		for (int k = lo + (int)dsb_lane(); k < hi; k += DSB_WV) ref[k] = DSB_STACK_PATTERN;
 		dsb_wsync();
 	}
+}
+template <bool WAVE>
+DSB_HD void dsb_fill_pattern(dsb_read_ws *w, uint8_t *ref, int lo, int hi)
+{
+	uint64_t t0 = DSB_T0();
+	dsb_fill_pattern_impl<WAVE>(ref, lo, hi);
+	DSB_T1(DSB_ST_T_FILL, t0);
 }
 
 #define DSB_S_A_KMER_L 9
@@ -1460,9 +1470,45 @@ DSB_HD void dsb_sc_hash_idx(dsb_read_ws *w)
 	}
 }
 
+/*
+ * Read 9-mer hash node (one u32 per read position, heads[key] = first position, EMPTY = none):
+ *   key_len < 18:  bits 0-23 next position with the same key (0xFFFFFF = none), bits 24-31 the
+ *                  k-mer bits above the key (kmer >> key_len, at most 8 bits)
+ *   key_len == 18: the next position (EMPTY = none); the key is the whole 18-bit k-mer
+ * (positions are < 2^17 whenever key_len < 18).  Equality with a probe k-mer whose key bits
+ * select the list is then (probe >> key_len) == stored high bits, which is also false for the
+ * unmasked probes (> 0x3ffff) of the backward scan, as in the reference's 64-bit compare.
+ */
+#define DSB_HEMPTY 0xffffffffu
+DSB_HD uint32_t dsb_hnode(uint32_t next, uint32_t kmer, int kl)
+{
+	return kl >= 18 ? next : ((next & 0xffffffu) | ((kmer >> kl) << 24));
+}
+DSB_HD uint32_t dsb_hnext(uint32_t node, int kl)
+{
+	if (kl >= 18)
+		return node;
+	uint32_t n = node & 0xffffffu;
+	return n == 0xffffffu ? DSB_HEMPTY : n;
+}
+DSB_HD int dsb_hmatch(uint32_t node, uint64_t kmer, int kl)
+{
+	return (kmer >> kl) == (uint64_t)(kl >= 18 ? 0u : (node >> 24));
+}
+
+/* the read 9-mer at c: kmer(c) = (OR_k q[c+k] << 2(8-k)) & 0x3ffff, the rolled value */
+DSB_HD uint32_t dsb_q9mer(const uint8_t *q)
+{
+	uint64_t a = dsb_ld8u(q), b = dsb_ld8u(q + 8);
+	uint32_t kmer = 0;
+	for (int k = 0; k < 8; k++) kmer = (kmer << 2) | (uint32_t)((a >> (8 * k)) & 0xff);
+	kmer = (kmer << 2) | (uint32_t)(b & 0xff);
+	return kmer & 0x3ffff;
+}
+
 /* build_hash_table_M2, src/cly.c:2168-2219: chained 9-mer hash of the read, per strand.
- * Chains keep insertion (= position) order, so heads/tails/next arrays reproduce the
- * reference's lookup order exactly. */
+ * Lists hold positions in increasing order (the reference appends in position order), built
+ * here from the last position backwards so that only the heads array is needed. */
 template <bool WAVE>
 DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 {
@@ -1483,60 +1529,43 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 		uint32_t direction = (c_dir == 1) ? DSB_REVERSE : DSB_FORWARD;
 		const dsb_sdir_t *csd = (w->sd[0].direction == direction) ? &w->sd[0] : &w->sd[1];
 		int h = (c_dir == 2) ? 0 : 1;
-		uint32_t *heads = w->hh[h], *tails = w->ht[h], *next = w->hn[h], *kk = w->hk[h];
+		uint32_t *heads = w->hh[h], *node = w->hn[h];
 		const uint8_t *q = w->bin + (csd->strand ? w->L : 0);
+		int n_pos = q_len - DSB_S_A_KMER_L + 1;
 		if (!WAVE || DSB_SEQ(w, 1)) {
-			for (uint32_t k = 0; k <= KEY_MASK; k++) heads[k] = 0xffffffffu;
-			uint32_t kmer = 0;
-			for (int k = 0; k < DSB_S_A_KMER_L - 1; k++) kmer = (kmer << 2) | q[k];
-			for (uint32_t c_pos = 0; c_pos < (uint32_t)(q_len - DSB_S_A_KMER_L + 1); c_pos++) {
-				kmer = ((kmer << 2) | q[c_pos + DSB_S_A_KMER_L - 1]) & 0x3ffff;
+			for (uint32_t k = 0; k <= KEY_MASK; k++) heads[k] = DSB_HEMPTY;
+			for (int c_pos = n_pos - 1; c_pos >= 0; c_pos--) {
+				uint32_t kmer = dsb_q9mer(q + c_pos);
 				uint32_t key = kmer & KEY_MASK;
-				kk[c_pos] = kmer;
-				next[c_pos] = 0xffffffffu;
-				if (heads[key] == 0xffffffffu) heads[key] = c_pos;
-				else next[tails[key]] = c_pos;
-				tails[key] = c_pos;
+				node[c_pos] = dsb_hnode(heads[key], kmer, key_len);
+				heads[key] = (uint32_t)c_pos;
 			}
 		} else {
-			/* Same lists as the sequential insertion: positions are linked in chunks of 64 in
-			 * position order; inside a chunk each lane finds its same-key neighbours by
-			 * shuffles.  kmer(c) = (OR_k q[c+k] << 2(8-k)) & 0x3ffff is the rolled value. */
+			/* chunks of 64 positions from the end; inside a chunk each lane finds the nearest
+			 * higher lane with its key (its list successor) and whether a lower lane has it */
 			uint32_t lane = dsb_lane();
-			for (uint32_t k = lane; k <= KEY_MASK; k += DSB_WV) heads[k] = 0xffffffffu;
+			for (uint32_t k = lane; k <= KEY_MASK; k += DSB_WV) heads[k] = DSB_HEMPTY;
 			if (w->stats && lane == 0) w->stats[DSB_ST_HASH_B] += 4ull * (KEY_MASK + 1);
 			dsb_wsync();
-			uint32_t n_pos = (uint32_t)(q_len - DSB_S_A_KMER_L + 1);
-			for (uint32_t cb = 0; cb < n_pos; cb += DSB_WV) {
-				uint32_t c_pos = cb + lane;
+			for (int cb = n_pos > 0 ? ((n_pos - 1) & ~(DSB_WV - 1)) : -1; cb >= 0; cb -= DSB_WV) {
+				int c_pos = cb + (int)lane;
 				int act = c_pos < n_pos;
-				uint32_t kmer = 0;
-				if (act)
-					for (int k = 0; k < DSB_S_A_KMER_L; k++) kmer = (kmer << 2) | q[c_pos + k];
-				kmer &= 0x3ffff;
+				uint32_t kmer = act ? dsb_q9mer(q + c_pos) : 0;
 				int key = act ? (int)(kmer & KEY_MASK) : -1 - (int)lane;
-				int prev = -1, nxt = -1;
-				for (int o = 0; o < DSB_WV; o++) {
+				int has_prev = 0, nxt = -1;
+				for (int o = DSB_WV - 1; o >= 0; o--) {
 					int k2 = dsb_wshfl(key, o);
 					if (k2 == key) {
-						if (o < (int)lane) prev = o;
-						else if (o > (int)lane && nxt < 0) nxt = o;
+						if (o < (int)lane) has_prev = 1;
+						else if (o > (int)lane) nxt = o;
 					}
-				}
-				uint32_t hd = 0, tl = 0;
-				if (act && prev < 0) {
-					hd = heads[key];
-					if (hd != 0xffffffffu) tl = tails[key];
 				}
 				if (act) {
-					if (w->stats) w->stats[DSB_ST_HASH_B] += 16;
-					kk[c_pos] = kmer;
-					next[c_pos] = (nxt >= 0) ? cb + (uint32_t)nxt : 0xffffffffu;
-					if (prev < 0) {
-						if (hd == 0xffffffffu) heads[key] = c_pos;
-						else next[tl] = c_pos;
-					}
-					if (nxt < 0) tails[key] = c_pos;
+					if (w->stats) w->stats[DSB_ST_HASH_B] += 12;
+					uint32_t succ = (nxt >= 0) ? (uint32_t)(cb + nxt) : heads[key];
+					node[c_pos] = dsb_hnode(succ, kmer, key_len);
+					if (!has_prev)
+						heads[key] = (uint32_t)c_pos;
 				}
 				dsb_wsync();
 			}
@@ -1569,19 +1598,6 @@ DSB_HD dsb_spd_t *dsb_push_sms(dsb_read_ws *w)
 }
 
 /* MEM_search, src/cly.c:1805-1813 */
-/* 8 bytes at p (any alignment) from the two aligned words covering them; may read up to 15
- * bytes past p, which stay inside the read's workspace arena (guards, or the next region). */
-DSB_HD uint64_t dsb_ld8u(const uint8_t *p)
-{
-	uintptr_t a = (uintptr_t)p;
-	const uint64_t *b = (const uint64_t *)(a & ~(uintptr_t)7);
-	uint32_t sh = (uint32_t)(a & 7) * 8;
-	uint64_t lo = b[0];
-	if (!sh)
-		return lo;
-	return (lo >> sh) | (b[1] << (64 - sh));
-}
-
 /* MEM_search: the byte loop `len < max && *q++ == *t++` (or `*q-- == *t--`) compared 8 bytes
  * per step: the first differing byte is the lowest (forward) / highest (backward) set byte of
  * the XOR.  Same result as the byte loop for every max >= 0. */
@@ -1620,7 +1636,7 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 	if (!WAVE || DSB_SEQ(w, 2)) {
 	uint32_t KEY_MASK = (1u << key_len) - 1;
 	uint32_t t_kmer_num = t_len - DSB_S_A_KMER_L + 1;
-	const uint32_t *heads = w->hh[hslot], *next = w->hn[hslot], *kk = w->hk[hslot];
+	const uint32_t *heads = w->hh[hslot], *hnode = w->hn[hslot];
 	if (isForward) {
 		const uint8_t *c_t_str = t_str + 4;
 		uint64_t kmer = 0;
@@ -1630,8 +1646,9 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			kmer = ((kmer << 2) | c_t_str[DSB_S_A_KMER_L - 1]) & 0x3ffff;
 			if ((i & 0x03) != 0)
 				continue;
-			for (uint32_t nd = heads[kmer & KEY_MASK]; nd != 0xffffffffu; nd = next[nd]) {
-				if (kk[nd] != (uint32_t)kmer)
+			for (uint32_t nd = heads[kmer & KEY_MASK], hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
+				hv = hnode[nd];
+				if (!dsb_hmatch(hv, kmer, key_len))
 					continue;
 				uint32_t q_pos = nd;
 				if (q_pos >= q_bg && q_pos <= q_ed) {
@@ -1662,8 +1679,9 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			kmer = (kmer >> 2) | ((uint64_t)c_t_str[0] << 16); /* bit2_preKmerMOVE, no mask */
 			if ((i & 0x03) != 0)
 				continue;
-			for (uint32_t nd = heads[kmer & KEY_MASK]; nd != 0xffffffffu; nd = next[nd]) {
-				if ((uint64_t)kk[nd] != kmer)
+			for (uint32_t nd = heads[kmer & KEY_MASK], hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
+				hv = hnode[nd];
+				if (!dsb_hmatch(hv, kmer, key_len))
 					continue;
 				uint32_t q_pos = nd;
 				if (q_pos >= q_bg && q_pos <= q_ed) {
@@ -1691,7 +1709,7 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 		int lim = (int)t_kmer_num;
 		if (lim <= 4)
 			return;
-		const uint32_t *heads = w->hh[hslot], *next = w->hn[hslot], *kk = w->hk[hslot];
+		const uint32_t *heads = w->hh[hslot], *hnode = w->hn[hslot];
 		int n_i = (lim - 1) >> 2; /* looked-up positions i = 4m, m = 1..n_i */
 		uint32_t lane = dsb_lane();
 		if (!dsb_win_ok(w, t_str, isForward ? 0 : -51, (int64_t)t_len + 64, 2))
@@ -1706,8 +1724,7 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			if (m <= n_i) {
 				if (isForward) { /* ((k << 2) | c) & 0x3ffff rolled: only the 9 bytes at i remain */
 					c_t_str = t_str + i;
-					for (int k = 0; k < DSB_S_A_KMER_L; k++) kmer = (kmer << 2) | c_t_str[k];
-					kmer &= 0x3ffff;
+					kmer = dsb_q9mer(c_t_str);
 				} else {
 					/* (k >> 2) | (c << 16) rolled without a mask: bytes > 3 (pattern/stale window
 					 * bytes, sdp_left's t_offset_global == 0 case) linger for up to 12 steps */
@@ -1722,9 +1739,10 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 						kmer |= ((uint64_t)t_str[(int)t_len - DSB_S_A_KMER_L - j] << 16) >> (2 * (i - j));
 				}
 				if (w->stats) w->stats[DSB_ST_LOOKUP]++;
-				for (uint32_t nd = heads[kmer & KEY_MASK]; nd != 0xffffffffu; nd = next[nd]) {
+				for (uint32_t nd = heads[kmer & KEY_MASK], hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
 					if (w->stats) w->stats[DSB_ST_NODE]++;
-					if (isForward ? (kk[nd] != (uint32_t)kmer) : ((uint64_t)kk[nd] != kmer))
+					hv = hnode[nd];
+					if (!dsb_hmatch(hv, kmer, key_len))
 						continue;
 					uint32_t q_pos = nd;
 					if (!(q_pos >= q_bg && q_pos <= q_ed))
@@ -1781,8 +1799,9 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			if (cnt > 1) { dsb_spd_t *d = dsb_sms(w, dst + 1); d->len = e1.len; d->q_pos = e1.q_pos; d->t_pos = e1.t_pos; }
 			if (cnt > 2) { /* rare: more than two matches for one position, walk the list again */
 				uint32_t k = 0;
-				for (uint32_t nd = heads[kmer & KEY_MASK]; nd != 0xffffffffu; nd = next[nd]) {
-					if (isForward ? (kk[nd] != (uint32_t)kmer) : ((uint64_t)kk[nd] != kmer))
+				for (uint32_t nd = heads[kmer & KEY_MASK], hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
+					hv = hnode[nd];
+					if (!dsb_hmatch(hv, kmer, key_len))
 						continue;
 					uint32_t q_pos = nd;
 					if (!(q_pos >= q_bg && q_pos <= q_ed))
@@ -1867,7 +1886,7 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 				dsb_get_ref_win<WAVE>(w, ref, (uint64_t)(int64_t)(pre_refoffset + pre_mch) + t_offset, (uint32_t)total_ref_len);
 				/* the reference re-initialises the whole ref[2000]; a forward scan of t_len bytes reads
 				 * at most ref[t_len + 58] (MEM_search bound t_len - i - 1 + OVER_SEARCH past i + 9) */
-				dsb_fill_pattern<WAVE>(ref, total_ref_len, DSB_MIN(total_ref_len + 64, 2000 + 64));
+				dsb_fill_pattern<WAVE>(w, ref, total_ref_len, DSB_MIN(total_ref_len + 64, 2000 + 64));
 				dsb_sdp_match<WAVE>(w, pre_a->index_in_read + pre_mch - 8, c_a->index_in_read - 1, q_str, ref,
 					      (uint32_t)total_ref_len, key_len, hslot, (uint32_t)(pre_refoffset + pre_mch), 1);
 				if (w->overflow) return 0;
@@ -1877,6 +1896,7 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 			p->q_pos = c_a->index_in_read;
 			p->t_pos = c_a->ref_offset;
 			p->len = c_a->mtch_len - DSB_S_A_KMER_L + 1;
+			uint64_t tdp0 = DSB_T0();
 			if (w->n_sms > 1) {
 				for (uint32_t cs = 1; cs < w->n_sms; cs++) {
 					dsb_spd_t *c_spd = dsb_sms(w, cs);
@@ -1914,6 +1934,7 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 					c_spd->score = (uint32_t)max_score;
 				}
 			}
+			DSB_T1(DSB_ST_T_DPM, tdp0);
 		} else
 			score += c_a->mtch_len - DSB_S_A_KMER_L + 1;
 		c_a_i = pre_i;
@@ -1966,7 +1987,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 	int32_t combined;
 	w->n_sms = 0;
 	uint8_t *ref = w->win + DSB_WIN_RL; /* uint8_t ref[1000] (src/cly.c:2537) */
-	dsb_fill_pattern<WAVE>(ref, -64, 1000 + 64); /* ref[-1] is read by sdp_left's back extension */
+	dsb_fill_pattern<WAVE>(w, ref, -64, 1000 + 64); /* ref[-1] is read by sdp_left's back extension */
 	dsb_spd_t *p = dsb_push_sms(w);
 	if (!p) return 0;
 	p->score = score_ori;
@@ -2009,6 +2030,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 		int max_score = (int)c_sms->len;
 		uint32_t max_pre_q = c_sms->q_pos + DSB_MAX_SMS_OVERLAP;
 		uint32_t max_pre_t = c_sms->t_pos + DSB_MAX_SMS_OVERLAP;
+		uint64_t tdp0 = DSB_T0();
 		if (!WAVE || DSB_SEQ(w, 4)) {
 			for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
 				dsb_spd_t *c_pre = dsb_sms(w, ps);
@@ -2068,6 +2090,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 			best = dsb_wmax(best);
 			max_score = DSB_MAX(max_score, best);
 		}
+		DSB_T1(DSB_ST_T_DPS, tdp0);
 		c_sms->score = (uint32_t)max_score;
 		if (c_sms->len >= 8 &&
 		    dsb_combine_chain(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 0, (int)c_sms->q_pos, &combined)) {
@@ -2113,7 +2136,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 	int32_t combined;
 	w->n_sms = 0;
 	uint8_t *ref = w->win + DSB_WIN_RL; /* uint8_t ref[1000] (src/cly.c:2683) */
-	dsb_fill_pattern<WAVE>(ref, -64, 1000 + 64); /* ref[-1] is read by sdp_left's back extension */
+	dsb_fill_pattern<WAVE>(w, ref, -64, 1000 + 64); /* ref[-1] is read by sdp_left's back extension */
 	dsb_spd_t *p = dsb_push_sms(w);
 	if (!p) return 0;
 	p->score = score_ori;
@@ -2158,6 +2181,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 		int max_score = (int)c_sms->len;
 		uint32_t min_pre_q = c_sms->q_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
 		uint32_t min_pre_t = c_sms->t_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
+		uint64_t tdp0 = DSB_T0();
 		if (!WAVE || DSB_SEQ(w, 4)) {
 			for (int64_t ps = (int64_t)current_sms - 2; ps >= 0; ps--) {
 				dsb_spd_t *c_pre = dsb_sms(w, ps);
@@ -2214,6 +2238,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 			best = dsb_wmax(best);
 			max_score = DSB_MAX(max_score, best);
 		}
+		DSB_T1(DSB_ST_T_DPS, tdp0);
 		c_sms->score = (uint32_t)max_score;
 		if (c_sms->len >= 8 && dsb_combine_chain(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 1,
 							 (int)(c_sms->q_pos + c_sms->len), &combined)) {

@@ -41,6 +41,19 @@
 #define DSB_STACK_PATTERN 0xAA
 #define DSB_HEAP_PERTURB 0x5A
 
+/* 8 bytes at p (any alignment) from the two aligned words covering them; may read up to 15
+ * bytes past p, which stay inside the read's workspace arena (guards, or the next region). */
+DSB_HD uint64_t dsb_ld8u(const uint8_t *p)
+{
+	uintptr_t a = (uintptr_t)p;
+	const uint64_t *b = (const uint64_t *)(a & ~(uintptr_t)7);
+	uint32_t sh = (uint32_t)(a & 7) * 8;
+	uint64_t lo = b[0];
+	if (!sh)
+		return lo;
+	return (lo >> sh) | (b[1] << (64 - sh));
+}
+
 /* ------------------------------------------------------------------ hashing */
 /* hash64_1, src/lib/utils.c:1067-1077 */
 DSB_HD uint64_t dsb_hash64_1(uint64_t key)

@@ -14,8 +14,9 @@ extern "C" {
 
 #define DSB_MAX_HITS 400 /* delete_small_score_rst keeps at most 400 chains (src/cly.c:2892) */
 
-#define DSB_N_STATS 160 /* 16 counters x (9 phases of part A + k_classB) */
-#define DSB_STATS_B 144
+#define DSB_ST_STRIDE 32 /* counters per phase */
+#define DSB_N_STATS 320 /* 32 counters x (9 phases of part A + k_classB) */
+#define DSB_STATS_B 288
 
 typedef struct {
 	double ms_total;      /* wall time of dsb_gpu_classify, host-measured */
@@ -24,7 +25,7 @@ typedef struct {
 	double ms_phase[12];  /* k_phase<ph> times (ms_classA = their sum) */
 	uint64_t n_reads, n_bases, n_retry, n_chunks;
 	uint64_t seed_positions; /* k-mer positions probed by the seed kernel (both strands) */
-	uint64_t stats[DSB_N_STATS]; /* work counters DSB_ST_*: [16*ph, 16*ph+16) phase ph, [144,160) k_classB */
+	uint64_t stats[DSB_N_STATS]; /* work counters DSB_ST_*: [32*ph, 32*ph+32) phase ph, [288,320) k_classB */
 } dsb_gpu_timing;
 
 /* Upload the index to `device` (-1: DSB_DEVICE env var, else the current HIP device).

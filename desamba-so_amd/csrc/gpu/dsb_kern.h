@@ -76,7 +76,7 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t 
 	}
 	if (STATS)
 		for (int k = 0; k < DSB_ST_N; k++)
-			atomicAdd(gstats + 16 * PH + k, (unsigned long long)st[k]);
+			atomicAdd(gstats + DSB_ST_STRIDE * PH + k, (unsigned long long)st[k]);
 }
 
 /* One phase of part A with one wavefront per read (dsb_wave.h), one wave per workgroup:
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 	if (STATS)
 		for (int k = 0; k < DSB_ST_N; k++)
 			if (st[k])
-				atomicAdd(gstats + 16 * PH + k, (unsigned long long)st[k]);
+				atomicAdd(gstats + DSB_ST_STRIDE * PH + k, (unsigned long long)st[k]);
 }
 
 

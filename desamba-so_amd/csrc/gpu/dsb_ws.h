@@ -60,7 +60,7 @@ DSB_HD dsb_ws_layout dsb_layout(uint32_t L, dsb_caps_t cap)
 	o.hit_tmp = p; p = dsb_al(p + sizeof(dsb_chain_t) * (uint64_t)cap.hit);
 	o.sms = p; p = dsb_al(p + sizeof(dsb_spd_t) * (uint64_t)cap.sms);
 	o.kl = (uint32_t)dsb_key_len(L);
-	o.hash = p; p = dsb_al(p + 2ull * (8ull * (1ull << o.kl) + 8ull * L));
+	o.hash = p; p = dsb_al(p + 2ull * (4ull * (1ull << o.kl) + 4ull * L)); /* per strand: heads + nodes */
 	o.sch = p; p = dsb_al(p + sizeof(dsb_sch_t) * (256 + 2 * 400 + 64));
 	o.win = p; p = dsb_al(p + DSB_WIN_BYTES);
 	o.mem = p; p = dsb_al(p + sizeof(dsb_mem_t) * 16 * 64); /* 16 MEM results per lane (slow seeding) */
@@ -96,9 +96,7 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 	uint64_t hs = 1ull << o.kl;
 	for (int s = 0; s < 2; s++) {
 		w->hh[s] = h; h += hs;
-		w->ht[s] = h; h += hs;
 		w->hn[s] = h; h += L;
-		w->hk[s] = h; h += L;
 	}
 	w->sch = (dsb_sch_t *)(base + o.sch);
 	w->win = base + o.win;

@@ -28,6 +28,7 @@
 
 #include "dsb_kern.h"
 #include "dsb_debug.h"
+static_assert(DSB_ST_N <= DSB_ST_STRIDE, "work counters per phase");
 
 #define HIP_OK(x)                                                                                    \
 	do {                                                                                         \

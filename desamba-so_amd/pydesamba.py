@@ -15,7 +15,9 @@ LIB_PATH = os.path.join(HERE, "lib", "libdesamba.so")
 FMT_SAM, FMT_SAM_FULL, FMT_DES, FMT_DES_FULL = 1, 2, 3, 4
 PHASES = ["island", "fast0", "fast1", "resolve_f", "slow0", "resolve_s0", "slow1", "resolve_s1", "delA"]
 ST_NAMES = ["occ", "occ_nib", "mem_search", "sa", "uni", "ref_pos", "getref_b", "anchor", "chain", "ek1", "ek2",
-            "hash_b", "lookup", "node", "t_mem", "t_map"]
+            "hash_b", "lookup", "node", "t_mem", "t_map", "t_build", "t_match", "t_win", "t_all", "t_dpm", "t_dps",
+            "t_fill"]
+ST_STRIDE = 32
 
 
 class Timing(C.Structure):
@@ -24,15 +26,15 @@ class Timing(C.Structure):
                 ("ms_classA", C.c_double), ("ms_classB", C.c_double), ("ms_phase", C.c_double * 12),
                 ("n_reads", C.c_uint64),
                 ("n_bases", C.c_uint64), ("n_retry", C.c_uint64), ("n_chunks", C.c_uint64),
-                ("seed_positions", C.c_uint64), ("stats", C.c_uint64 * 160)]
+                ("seed_positions", C.c_uint64), ("stats", C.c_uint64 * 320)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("stats", "pad", "ms_phase")}
         d["ms_phase"] = {n: float(self.ms_phase[i]) for i, n in enumerate(PHASES)}
-        d["stats_phase"] = {ph: {n: int(self.stats[16 * p + i]) for i, n in enumerate(ST_NAMES)}
+        d["stats_phase"] = {ph: {n: int(self.stats[ST_STRIDE * p + i]) for i, n in enumerate(ST_NAMES)}
                             for p, ph in enumerate(PHASES)}
         d["stats"] = {n: sum(v[n] for v in d["stats_phase"].values()) for n in ST_NAMES}
-        d["stats_B"] = {n: int(self.stats[144 + i]) for i, n in enumerate(ST_NAMES)}
+        d["stats_B"] = {n: int(self.stats[ST_STRIDE * 9 + i]) for i, n in enumerate(ST_NAMES)}
         return d
 
 
