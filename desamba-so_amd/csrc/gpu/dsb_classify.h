@@ -523,6 +523,14 @@ DSB_HD uint32_t dsb_get_uni_w(dsb_read_ws *w, uint64_t bwt_pos, int search_l, ui
 	return u;
 }
 
+/* dst[k] = end[-k] for k < n (n <= 16), from two word loads (the read buffer has guards) */
+DSB_HD void dsb_rev_copy(uint8_t *dst, const uint8_t *end, uint32_t n)
+{
+	uint64_t a = dsb_ld8u(end - 7), b = dsb_ld8u(end - 15);
+	for (uint32_t k = 0; k < n; k++)
+		dst[k] = (uint8_t)((k < 8 ? (a >> (8 * (7 - k))) : (b >> (8 * (15 - k)))) & 0xff);
+}
+
 /* get_new_ed, src/cly.c:624-689 */
 DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t *len_, uint32_t *l_mem_ext,
 			    int32_t q_off, uint64_t t_off, uint32_t l_read, int is_FWD)
@@ -536,8 +544,7 @@ DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t
 			q_off = 0;
 		max_len = q_off;
 		len = DSB_MIN(12u, max_len);
-		for (uint8_t k = 0; k < len; k++)
-			q[k] = q_b[q_off - k];
+		dsb_rev_copy(q, q_b + q_off, len);
 	} else {
 		max_len = l_read - q_off;
 		len = DSB_MIN(12u, max_len);
@@ -557,8 +564,7 @@ DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t
 				if (is_FWD) {
 					q_off -= mtc;
 					t_off -= mtc;
-					for (uint8_t k = 0; k < len; k++)
-						q[k] = q_b[q_off - k];
+					dsb_rev_copy(q, q_b + q_off, len);
 				} else {
 					t_off += mtc;
 					q += mtc;
@@ -614,8 +620,7 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 	do {
 		uint8_t *q_suf;
 		l_pre = DSB_MIN(q_off + 1, DSB_LV_L);
-		for (uint8_t k = 0; k < l_pre; k++)
-			q_pre[k] = q_b[q_off - k];
+		dsb_rev_copy(q_pre, q_b + q_off, l_pre);
 		int s_l = 0;
 		if (m_r->sa_sp != ~0ull) {
 			uni = (int32_t)dsb_get_uni_w(w, m_r->sa_sp, m_r->sa_sp_l, &t_off, &u_off);

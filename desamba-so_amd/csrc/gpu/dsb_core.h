@@ -110,6 +110,26 @@ DSB_HD uint8_t dsb_cly_bit(uint8_t c)
  * value of bases s[0..l-1] (first base high), 0 when any base count >= single_base_max. */
 DSB_HD uint64_t dsb_kmer_at(const uint8_t *s, int l, int single_base_max)
 {
+	if (l <= 24) { /* three word loads; base counts packed 8 bits each */
+		uint64_t wv0 = dsb_ld8u(s), wv1 = dsb_ld8u(s + 8), wv2 = dsb_ld8u(s + 16);
+		uint64_t v = 0;
+		uint32_t pc = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+		for (int i = 0; i < 24; i++) {
+			if (i < l) {
+				uint64_t wd = i < 8 ? wv0 : (i < 16 ? wv1 : wv2);
+				uint32_t b = (uint32_t)(wd >> (8 * (i & 7))) & 0xff;
+				v = (v << 2) | b;
+				pc += 1u << (8 * (b & 3));
+			}
+		}
+		uint32_t m = (uint32_t)single_base_max;
+		if ((pc & 0xff) >= m || ((pc >> 8) & 0xff) >= m || ((pc >> 16) & 0xff) >= m || (pc >> 24) >= m)
+			return 0;
+		return v;
+	}
 	int cnt[4] = {0, 0, 0, 0};
 	uint64_t v = 0;
 	for (int i = 0; i < l; i++) {
@@ -241,6 +261,27 @@ DSB_HD uint8_t dsb_ref_byte(const dsb_dindex_t *ix, uint64_t off)
 DSB_HD void dsb_get_ref(const dsb_dindex_t *ix, uint8_t *ref_str, uint64_t uni_offset, uint32_t length,
 			 int isForward)
 {
+	if (length <= 28) { /* one 8-byte window of the packed reference (32 bases, MSB first) */
+		if (isForward) {
+			uint64_t B = uni_offset >> 2;
+			if (B + 16 <= ix->ref_bin_padded) {
+				uint64_t v = __builtin_bswap64(dsb_ld8u(ix->ref_bin + B));
+				uint32_t m0 = (uint32_t)(uni_offset & 3);
+				for (uint32_t k = 0; k < length; k++)
+					ref_str[k] = (uint8_t)((v >> (62 - 2 * (m0 + k))) & 3);
+				return;
+			}
+		} else {
+			uint64_t Be = uni_offset >> 2;
+			if (Be >= 7 && Be + 9 <= ix->ref_bin_padded) {
+				uint64_t v = __builtin_bswap64(dsb_ld8u(ix->ref_bin + Be - 7));
+				uint32_t m0 = (uint32_t)(uni_offset & 3) + 28;
+				for (uint32_t k = 0; k < length; k++)
+					ref_str[k] = (uint8_t)((v >> (62 - 2 * (m0 - k))) & 3);
+				return;
+			}
+		}
+	}
 	uint64_t offset = uni_offset >> 2;
 	uint8_t odd = uni_offset & 0x3;
 	if (isForward) {
