@@ -523,6 +523,16 @@ DSB_HD uint32_t dsb_get_uni_w(dsb_read_ws *w, uint64_t bwt_pos, int search_l, ui
 	return u;
 }
 
+/* dst[0..32) = src[0..32) (word loads) */
+DSB_HD void dsb_copy32(uint8_t *dst, const uint8_t *src)
+{
+	for (int k = 0; k < 4; k++) {
+		uint64_t v = dsb_ld8u(src + 8 * k);
+		for (int b = 0; b < 8; b++)
+			dst[8 * k + b] = (uint8_t)(v >> (8 * b));
+	}
+}
+
 /* dst[k] = end[-k] for k < n (n <= 16), from two word loads (the read buffer has guards) */
 DSB_HD void dsb_rev_copy(uint8_t *dst, const uint8_t *end, uint32_t n)
 {
@@ -572,6 +582,10 @@ DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t
 				dsb_get_ref_w(w, t, t_off, len, !is_FWD);
 			}
 		} while (mtc > 0);
+	}
+	if (!is_FWD) { /* lv_extd writes its terminator at q[len]: work on a private copy (lanes share the read) */
+		dsb_copy32(qbuf, q - 8);
+		q = qbuf + 8;
 	}
 	*e_d = dsb_lv_extd(t, len, q, len);
 	*len_ = len;
@@ -689,7 +703,9 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 					}
 				} while (mtc > 0);
 			}
-			d_suf = dsb_lv_extd(t_suf, l_suf, q_suf, l_suf);
+			uint8_t qsuf_b[32]; /* private copy: lv_extd writes its terminator at q_suf[l_suf] */
+			dsb_copy32(qsuf_b, q_suf - 8);
+			d_suf = dsb_lv_extd(t_suf, l_suf, qsuf_b + 8, l_suf);
 			s += Q_LV[d_suf * DSB_LV_DIM + l_suf];
 		} else
 			l_suf = d_suf = 0;
