@@ -122,7 +122,7 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
 				hset[k] = 0;
 			__syncthreads();
-			dsb_fast_classify_wave(&w, &w.sd[ph - DSB_PH_FAST0], hset);
+			dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset);
 		} else if (ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) {
 			uint64_t *hset = (uint64_t *)(base + lay.hset);
 			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
