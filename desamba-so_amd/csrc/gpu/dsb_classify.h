@@ -612,8 +612,22 @@ DSB_HD dsb_anchor_t *dsb_push_anchor(dsb_read_ws *w)
 #define DSB_LV_L 12
 #define DSB_MIN_S_1 12
 #define DSB_MIN_S_2 20
-/* map_seed, src/cly.c:701-934 */
-DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i)
+/* map_seed, src/cly.c:701-934, in two parts: dsb_map_seed_pre (locate the hit, extend and
+ * score its prefix / suffix: src/cly.c:701-884) leaves the REF_POS list of the hit's unitig in
+ * a context; dsb_map_item scores one REF_POS entry of it into an Anchor (src/cly.c:886-931).
+ * dsb_map_seed runs both in sequence; the wave seeding spreads the items over its lanes. */
+typedef struct {
+	uint64_t rp_s;          /* first REF_POS entry of the unitig */
+	uint32_t n_items;       /* REF_POS entries to score (0: none) */
+	int32_t ret;            /* map_seed's value when n_items == 0 */
+	int32_t q_off;
+	uint32_t l_m, u_off;
+	uint16_t am_mtch;
+	int16_t am_score;
+	uint8_t am_ll, am_le, am_rl, am_re, ref_l, ref_r;
+} dsb_mapctx_t;
+
+DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i, dsb_mapctx_t *cx)
 {
 	const dsb_dindex_t *ix = w->ix;
 	const int *Q_LV = ix->Q_LV;
@@ -715,63 +729,93 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 		}
 	} while (0);
 
+	cx->n_items = 0;
+	cx->ret = 0;
+	cx->q_off = q_off;
+	cx->l_m = l_m;
+	cx->u_off = u_off;
 	if (s > 0) {
 		/* Anchor_map a_m = {l_m, s, l_pre, d_pre, l_suf, d_suf} (uint16/int16/uint8 fields) */
-		uint16_t am_mtch = (uint16_t)l_m;
-		int16_t am_score = (int16_t)s;
-		uint8_t am_ll = (uint8_t)l_pre, am_le = (uint8_t)d_pre, am_rl = (uint8_t)l_suf, am_re = (uint8_t)d_suf;
+		cx->am_mtch = (uint16_t)l_m;
+		cx->am_score = (int16_t)s;
+		cx->am_ll = (uint8_t)l_pre; cx->am_le = (uint8_t)d_pre; cx->am_rl = (uint8_t)l_suf; cx->am_re = (uint8_t)d_suf;
 		uint64_t rp_s = ix->uni[uni].ref_list, rp_e = ix->uni[uni + 1].ref_list;
-		int ref_search_l = (l_pre < DSB_LV_L || d_pre == 0);
-		int ref_search_r = (l_suf < DSB_LV_L || d_suf == 0);
-		uint8_t duplicate = 0;
-		if (rp_e - rp_s > 50) {
-			if (!(rp_e - rp_s < 1000))
-				return 50;
+		cx->ref_l = (uint8_t)(l_pre < DSB_LV_L || d_pre == 0);
+		cx->ref_r = (uint8_t)(l_suf < DSB_LV_L || d_suf == 0);
+		if (rp_e - rp_s > 50 && !(rp_e - rp_s < 1000)) {
+			cx->ret = 50;
+			return;
 		}
-		for (uint64_t c_r_p = rp_s; c_r_p < rp_e; c_r_p++) {
-			uint64_t rp = ix->r_p[c_r_p];
-			if (w->stats) w->stats[DSB_ST_REFPOS]++;
-			uint32_t ed_l, ed_r, len_l, len_r;
-			uint32_t l_m_ext_l = 0, l_m_ext_r;
-			if (ref_search_l || ref_search_r) {
-				if (ref_search_l) {
-					dsb_get_new_ed(w, q_b, &ed_l, &len_l, &l_m_ext_l, q_off, DSB_RP_OFF(rp) + u_off - 1, s_i->read_L, 1);
-					am_ll = (uint8_t)len_l;
-					am_le = (uint8_t)ed_l;
-				}
-				am_mtch = (uint16_t)(l_m + l_m_ext_l);
-				if (ref_search_r) {
-					l_m_ext_r = 0;
-					dsb_get_new_ed(w, q_b, &ed_r, &len_r, &l_m_ext_r, q_off + l_m + 1, DSB_RP_OFF(rp) + u_off + l_m,
-						       s_i->read_L, 0);
-					am_rl = (uint8_t)len_r;
-					am_re = (uint8_t)ed_r;
-					am_mtch = (uint16_t)(am_mtch + l_m_ext_r);
-				}
-				am_score = (int16_t)(dsb_qmem(ix, am_mtch) + Q_LV[am_le * DSB_LV_DIM + am_ll] +
-						     Q_LV[am_re * DSB_LV_DIM + am_rl]);
-				if (am_score < DSB_MIN_S_2)
-					continue;
-			}
-			max_s = DSB_MAX(max_s, (int32_t)am_score);
-			dsb_anchor_t *a = dsb_push_anchor(w);
-			if (!a)
-				return max_s;
-			if (w->stats) w->stats[DSB_ST_ANCHOR]++;
-			a->direction = (uint8_t)s_i->direction;
-			a->index_in_read = q_off + 1 - l_m_ext_l;
-			a->global_offset = DSB_RP_OFF(rp) + u_off - l_m_ext_l;
-			a->ref_ID = DSB_RP_REF(rp);
-			a->ref_offset = (uint32_t)(a->global_offset - ix->ref_seq_offset[a->ref_ID]);
-			a->mtch_len = am_mtch;
-			a->score = am_score;
-			a->left_len = am_ll; a->left_ED = am_le; a->rigt_len = am_rl; a->rigt_ED = am_re;
-			a->seed_ID = s_i->seed_ID;
-			a->duplicate = duplicate;
-			a->pre = -1;
-			a->chain_id = 0;
-			a->anchor_useless = 0;
+		cx->rp_s = rp_s;
+		cx->n_items = (uint32_t)(rp_e - rp_s);
+	}
+}
+
+/* REF_POS entry rp_s + item of a hit: 1 and the Anchor in *a when the reference pushes one */
+DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, const dsb_seedinfo_t *s_i, dsb_anchor_t *a)
+{
+	const dsb_dindex_t *ix = w->ix;
+	const int *Q_LV = ix->Q_LV;
+	uint64_t rp = ix->r_p[cx->rp_s + item];
+	if (w->stats) w->stats[DSB_ST_REFPOS]++;
+	uint16_t am_mtch = cx->am_mtch;
+	int16_t am_score = cx->am_score;
+	uint8_t am_ll = cx->am_ll, am_le = cx->am_le, am_rl = cx->am_rl, am_re = cx->am_re;
+	uint32_t ed_l, ed_r, len_l, len_r;
+	uint32_t l_m_ext_l = 0, l_m_ext_r;
+	if (cx->ref_l || cx->ref_r) {
+		if (cx->ref_l) {
+			dsb_get_new_ed(w, s_i->bin_read, &ed_l, &len_l, &l_m_ext_l, cx->q_off, DSB_RP_OFF(rp) + cx->u_off - 1,
+				       s_i->read_L, 1);
+			am_ll = (uint8_t)len_l;
+			am_le = (uint8_t)ed_l;
 		}
+		am_mtch = (uint16_t)(cx->l_m + l_m_ext_l);
+		if (cx->ref_r) {
+			l_m_ext_r = 0;
+			dsb_get_new_ed(w, s_i->bin_read, &ed_r, &len_r, &l_m_ext_r, cx->q_off + cx->l_m + 1,
+				       DSB_RP_OFF(rp) + cx->u_off + cx->l_m, s_i->read_L, 0);
+			am_rl = (uint8_t)len_r;
+			am_re = (uint8_t)ed_r;
+			am_mtch = (uint16_t)(am_mtch + l_m_ext_r);
+		}
+		am_score = (int16_t)(dsb_qmem(ix, am_mtch) + Q_LV[am_le * DSB_LV_DIM + am_ll] + Q_LV[am_re * DSB_LV_DIM + am_rl]);
+		if (am_score < DSB_MIN_S_2)
+			return 0;
+	}
+	a->direction = (uint8_t)s_i->direction;
+	a->index_in_read = cx->q_off + 1 - l_m_ext_l;
+	a->global_offset = DSB_RP_OFF(rp) + cx->u_off - l_m_ext_l;
+	a->ref_ID = DSB_RP_REF(rp);
+	a->ref_offset = (uint32_t)(a->global_offset - ix->ref_seq_offset[a->ref_ID]);
+	a->mtch_len = am_mtch;
+	a->score = am_score;
+	a->left_len = am_ll; a->left_ED = am_le; a->rigt_len = am_rl; a->rigt_ED = am_re;
+	a->seed_ID = s_i->seed_ID;
+	a->duplicate = 0;
+	a->pre = -1;
+	a->chain_id = 0;
+	a->anchor_useless = 0;
+	return 1;
+}
+
+DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i)
+{
+	dsb_mapctx_t cx;
+	dsb_map_seed_pre(w, m_r, s_i, &cx);
+	if (cx.n_items == 0)
+		return cx.ret;
+	int32_t max_s = 0;
+	for (uint32_t it = 0; it < cx.n_items; it++) {
+		dsb_anchor_t an;
+		if (!dsb_map_item(w, &cx, it, s_i, &an))
+			continue;
+		max_s = DSB_MAX(max_s, (int32_t)an.score);
+		dsb_anchor_t *a = dsb_push_anchor(w);
+		if (!a)
+			return max_s;
+		if (w->stats) w->stats[DSB_ST_ANCHOR]++;
+		*a = an;
 	}
 	return max_s;
 }
@@ -1070,15 +1114,90 @@ DSB_HDN void dsb_fast_classify_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_
 			break;
 		uint64_t mapm = dsb_wballot(st == DSB_SM_MAP);
 		int do_map = mapm != 0 && ((uint32_t)__builtin_popcountll(mapm) >= DSB_SM_MAP_BATCH || mapm == act);
-		/* ---- MAP: map_seed of hit k_map, batched */
-		if (st == DSB_SM_MAP && do_map) {
-			m_r[k_map].read_offset = string_index - m_r[k_map].match_len;
-			dsb_seedinfo_t s_i = {bin_read, w->L, (uint16_t)ci, s_d->direction};
+		/* ---- MAP: map_seed of hit k_map, batched; its REF_POS entries are spread over the wave.
+		 * Items are numbered owner by owner (lane order), REF_POS order inside an owner; a kept
+		 * Anchor goes to its owner's staging at the owner's count + the number of kept items of
+		 * that owner before it, i.e. the order of the reference's loop (src/cly.c:886-931). */
+		if (do_map) {
 			uint64_t t1 = w->stats ? dsb_clock() : 0;
-			int c_score = dsb_map_seed(w, m_r + k_map, &s_i);
-			if (w->stats) w->stats[DSB_ST_T_MAP] += dsb_clock() - t1;
-			max_score = DSB_MAX(c_score, max_score);
-			k_map++;
+			int inmap = st == DSB_SM_MAP;
+			dsb_mapctx_t cx;
+			cx.n_items = 0;
+			cx.ret = 0;
+			dsb_seedinfo_t s_i = {bin_read, w->L, (uint16_t)ci, s_d->direction};
+			if (inmap) {
+				m_r[k_map].read_offset = string_index - m_r[k_map].match_len;
+				dsb_map_seed_pre(w, m_r + k_map, &s_i, &cx);
+			}
+			uint32_t cnt = inmap ? cx.n_items : 0;
+			uint32_t tot, pfx = dsb_wscan(cnt, &tot);
+			uint32_t n_before = w->n_anc;
+			for (uint32_t cb = 0; cb < tot; cb += DSB_WV) {
+				uint32_t it = cb + lane;
+				int o = 0; /* owner: the last lane whose prefix is <= it */
+				for (int step = DSB_WV / 2; step > 0; step >>= 1)
+					if ((uint32_t)dsb_wshfl_any((int)pfx, o + step) <= it)
+						o += step;
+				dsb_mapctx_t oc;
+				uint32_t opfx = (uint32_t)dsb_wshfl_any((int)pfx, o);
+				oc.rp_s = ((uint64_t)(uint32_t)dsb_wshfl_any((int)(uint32_t)(cx.rp_s >> 32), o) << 32) |
+					  (uint32_t)dsb_wshfl_any((int)(uint32_t)cx.rp_s, o);
+				oc.q_off = dsb_wshfl_any(cx.q_off, o);
+				oc.l_m = (uint32_t)dsb_wshfl_any((int)cx.l_m, o);
+				oc.u_off = (uint32_t)dsb_wshfl_any((int)cx.u_off, o);
+				uint32_t pk1 = (uint32_t)cx.am_mtch | ((uint32_t)(uint16_t)cx.am_score << 16);
+				uint32_t pk2 = (uint32_t)cx.am_ll | ((uint32_t)cx.am_le << 8) | ((uint32_t)cx.am_rl << 16) |
+					       ((uint32_t)cx.am_re << 24);
+				uint32_t pk3 = (uint32_t)cx.ref_l | ((uint32_t)cx.ref_r << 1) | ((ci & 0xffffu) << 16);
+				pk1 = (uint32_t)dsb_wshfl_any((int)pk1, o);
+				pk2 = (uint32_t)dsb_wshfl_any((int)pk2, o);
+				pk3 = (uint32_t)dsb_wshfl_any((int)pk3, o);
+				uint32_t o_n = (uint32_t)dsb_wshfl_any((int)n_before, o);
+				oc.am_mtch = (uint16_t)pk1;
+				oc.am_score = (int16_t)(pk1 >> 16);
+				oc.am_ll = (uint8_t)pk2; oc.am_le = (uint8_t)(pk2 >> 8); oc.am_rl = (uint8_t)(pk2 >> 16);
+				oc.am_re = (uint8_t)(pk2 >> 24);
+				oc.ref_l = (uint8_t)(pk3 & 1);
+				oc.ref_r = (uint8_t)((pk3 >> 1) & 1);
+				dsb_seedinfo_t os = {bin_read, w->L, (uint16_t)(pk3 >> 16), s_d->direction};
+				dsb_anchor_t an;
+				int pass = it < tot ? dsb_map_item(w, &oc, it - opfx, &os, &an) : 0;
+				uint64_t pm = dsb_wballot(pass);
+				uint32_t start = opfx > cb ? opfx - cb : 0; /* the owner's first item in this chunk */
+				uint64_t before = (lane == 0 ? 0 : (~0ull >> (64 - lane))) & ~(start == 0 ? 0 : (~0ull >> (64 - start)));
+				uint32_t dest = o_n + (uint32_t)__builtin_popcountll(pm & before);
+				if (pass && dest < S) {
+					w->anc_tmp[(uint64_t)o * S + dest] = an;
+					if (w->stats) w->stats[DSB_ST_ANCHOR]++;
+				}
+				/* owners: count their kept items of this chunk */
+				if (inmap) {
+					uint32_t lo = pfx > cb ? pfx - cb : 0, hi = DSB_MIN(pfx + cnt, cb + DSB_WV) - cb;
+					if (pfx + cnt > cb && lo < hi) {
+						uint64_t mine = (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & ~(lo == 0 ? 0ull : ((1ull << lo) - 1));
+						n_before += (uint32_t)__builtin_popcountll(pm & mine);
+					}
+				}
+			}
+			dsb_wsync();
+			if (inmap) {
+				int c_score = cx.ret;
+				if (cx.n_items) { /* max over the kept anchors (the reference's max_s) */
+					if (n_before > S) {
+						w->overflow |= 1;
+						n_before = S;
+					}
+					c_score = 0;
+					for (uint32_t a = w->n_anc; a < n_before; a++)
+						c_score = DSB_MAX(c_score, (int)stg[a].score);
+					w->n_anc = n_before;
+				}
+				if (w->stats) w->stats[DSB_ST_T_MAP] += dsb_clock() - t1;
+				max_score = DSB_MAX(c_score, max_score);
+				k_map++;
+			}
+		}
+		if (st == DSB_SM_MAP && do_map) {
 			if (k_map == n_m) {
 				if (w->overflow) {
 					st = DSB_SM_FIN;

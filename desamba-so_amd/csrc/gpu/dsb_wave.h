@@ -61,6 +61,8 @@ DSB_HD uint64_t dsb_wmax64(uint64_t v)
 	return v;
 }
 DSB_HD uint64_t dsb_wballot(int p) { return __ballot(p); }
+/* value of lane `src` for a per-lane src (ds_bpermute) */
+DSB_HD int dsb_wshfl_any(int v, int src) { return __shfl(v, src); }
 /* value of lane `src`; src must be wave-uniform (v_readlane) */
 DSB_HD int dsb_wshfl(int v, int src) { return dsb_rdlane(v, src); }
 #else
@@ -72,6 +74,7 @@ DSB_HD uint32_t dsb_wscan(uint32_t v, uint32_t *tot) { *tot = v; return 0; }
 DSB_HD uint64_t dsb_wmax64(uint64_t v) { return v; }
 DSB_HD uint64_t dsb_wballot(int p) { return p ? 1 : 0; }
 DSB_HD int dsb_wshfl(int v, int src) { (void)src; return v; }
+DSB_HD int dsb_wshfl_any(int v, int src) { (void)src; return v; }
 #endif
 
 #endif
