@@ -1043,427 +1043,6 @@ DSB_HDN void dsb_fast_classify_wave(dsb_read_ws *w, const dsb_sdir_t *s_d, uint6
 #endif
 enum { DSB_SM_J = 0, DSB_SM_EXT, DSB_SM_ROW, DSB_SM_SS, DSB_SM_MAP, DSB_SM_FIN, DSB_SM_DONE };
 
-DSB_HDN void dsb_fast_classify_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset)
-{
-	const dsb_dindex_t *ix = w->ix;
-	uint32_t lane = dsb_lane();
-	uint32_t n_sv = s_d->l_seed_v_f;
-	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV; /* dbg 32: tiny staging (tests the replay) */
-	dsb_anchor_t *stg = w->anc_tmp + (uint64_t)lane * S;
-	dsb_hset_t hs = {hset + lane, DSB_WV, 0, 0, 500};
-	uint8_t l_ek = (uint8_t)ix->l_ek;
-	int min_index = DSB_MIN_MEM_LEN_FAST - l_ek;
-	uint8_t *bin_read = w->bin + (s_d->strand ? w->L : 0);
-	/* ---- top seeds, in order (tix) */
-	uint32_t *tix = w->sidx, *rec = w->stmp;
-	uint32_t m = 0;
-	for (uint32_t gb = 0; gb < n_sv; gb += DSB_WV) {
-		uint32_t ci = gb + lane;
-		int t = ci < n_sv && w->seeds[s_d->seed_off + ci].top != 0;
-		uint64_t bm = dsb_wballot(t);
-		uint64_t below = (lane == 0) ? 0 : (bm & (~0ull >> (64 - lane)));
-		if (t)
-			tix[m + (uint32_t)__builtin_popcountll(below)] = ci;
-		m += (uint32_t)__builtin_popcountll(bm);
-	}
-	dsb_wsync();
-	if (m == 0)
-		return;
-	/* ---- the lane's anchor vector is its staging area while seeds run */
-	dsb_anchor_t *anc0 = w->anc;
-	uint32_t n0 = w->n_anc, cap0 = w->cap.anc, of0 = w->overflow;
-	w->anc = stg;
-	w->n_anc = 0;
-	w->cap.anc = S;
-	w->overflow = 0;
-	/* ---- per-lane seed state; every record starts as "overflowed" (replayed if never written) */
-	for (uint32_t q = lane; q < m; q += DSB_WV) {
-		rec[2 * q] = 0;
-		rec[2 * q + 1] = 1u << 30;
-	}
-	dsb_wsync();
-	uint32_t next_k = DSB_MIN((uint32_t)DSB_WV, m); /* next top seed to hand out (uniform) */
-	uint32_t k = lane;                                /* my top-seed index */
-	int st = DSB_SM_DONE;
-	uint32_t ci = 0, a_b = 0, seed_off = 0;
-	int j = 0, skip = 0, n_m = 0, k_map = 0, max_score = 0, string_index = 0, match_len = 0, row_single = 0;
-	uint64_t sp = 0, ep = 0, row = 0, row_end = 0, ss_sp = 0, sa_sp = 0;
-	int ss_len = 0, ss_max = 0, sa_sp_l = 0, l_max = 0;
-	const uint8_t *str = bin_read, *ss_str = bin_read;
-	dsb_mem_t m_r[DSB_MEM_SEARCH_FAST];
-	for (int q = 0; q < DSB_MEM_SEARCH_FAST; q++) {
-		m_r[q].match_len = 0; m_r[q].sp = 0; m_r[q].sa_sp = 0; m_r[q].sa_sp_l = 0; m_r[q].kmer_index = 0; m_r[q].read_offset = 0;
-	}
-#define DSB_SM_START_SEED(K)                                                   \
-	do {                                                                   \
-		k = (K);                                                       \
-		ci = tix[k];                                                   \
-		const dsb_seed_t *c_sv_ = w->seeds + s_d->seed_off + ci;       \
-		seed_off = c_sv_->offset;                                      \
-		j = (int)c_sv_->len - 1;                                       \
-		skip = 0;                                                      \
-		a_b = w->n_anc;                                                \
-		dsb_set_reset(&hs);                                            \
-		st = DSB_SM_J;                                                 \
-	} while (0)
-	if (k < m)
-		DSB_SM_START_SEED(lane);
-	for (;;) {
-		uint64_t act = dsb_wballot(st != DSB_SM_DONE);
-		if (!act)
-			break;
-		uint64_t mapm = dsb_wballot(st == DSB_SM_MAP);
-		int do_map = mapm != 0 && ((uint32_t)__builtin_popcountll(mapm) >= DSB_SM_MAP_BATCH || mapm == act);
-		/* ---- MAP: map_seed of hit k_map, batched; its REF_POS entries are spread over the wave.
-		 * Items are numbered owner by owner (lane order), REF_POS order inside an owner; a kept
-		 * Anchor goes to its owner's staging at the owner's count + the number of kept items of
-		 * that owner before it, i.e. the order of the reference's loop (src/cly.c:886-931). */
-		if (do_map) {
-			uint64_t t1 = w->stats ? dsb_clock() : 0;
-			int inmap = st == DSB_SM_MAP;
-			dsb_mapctx_t cx;
-			cx.n_items = 0;
-			cx.ret = 0;
-			dsb_seedinfo_t s_i = {bin_read, w->L, (uint16_t)ci, s_d->direction};
-			if (inmap) {
-				m_r[k_map].read_offset = string_index - m_r[k_map].match_len;
-				dsb_map_seed_pre(w, m_r + k_map, &s_i, &cx);
-			}
-			uint32_t cnt = inmap ? cx.n_items : 0;
-			uint32_t tot, pfx = dsb_wscan(cnt, &tot);
-			uint32_t n_before = w->n_anc;
-			for (uint32_t cb = 0; cb < tot; cb += DSB_WV) {
-				uint32_t it = cb + lane;
-				int o = 0; /* owner: the last lane whose prefix is <= it */
-				for (int step = DSB_WV / 2; step > 0; step >>= 1)
-					if ((uint32_t)dsb_wshfl_any((int)pfx, o + step) <= it)
-						o += step;
-				dsb_mapctx_t oc;
-				uint32_t opfx = (uint32_t)dsb_wshfl_any((int)pfx, o);
-				oc.rp_s = ((uint64_t)(uint32_t)dsb_wshfl_any((int)(uint32_t)(cx.rp_s >> 32), o) << 32) |
-					  (uint32_t)dsb_wshfl_any((int)(uint32_t)cx.rp_s, o);
-				oc.q_off = dsb_wshfl_any(cx.q_off, o);
-				oc.l_m = (uint32_t)dsb_wshfl_any((int)cx.l_m, o);
-				oc.u_off = (uint32_t)dsb_wshfl_any((int)cx.u_off, o);
-				uint32_t pk1 = (uint32_t)cx.am_mtch | ((uint32_t)(uint16_t)cx.am_score << 16);
-				uint32_t pk2 = (uint32_t)cx.am_ll | ((uint32_t)cx.am_le << 8) | ((uint32_t)cx.am_rl << 16) |
-					       ((uint32_t)cx.am_re << 24);
-				uint32_t pk3 = (uint32_t)cx.ref_l | ((uint32_t)cx.ref_r << 1) | ((ci & 0xffffu) << 16);
-				pk1 = (uint32_t)dsb_wshfl_any((int)pk1, o);
-				pk2 = (uint32_t)dsb_wshfl_any((int)pk2, o);
-				pk3 = (uint32_t)dsb_wshfl_any((int)pk3, o);
-				uint32_t o_n = (uint32_t)dsb_wshfl_any((int)n_before, o);
-				oc.am_mtch = (uint16_t)pk1;
-				oc.am_score = (int16_t)(pk1 >> 16);
-				oc.am_ll = (uint8_t)pk2; oc.am_le = (uint8_t)(pk2 >> 8); oc.am_rl = (uint8_t)(pk2 >> 16);
-				oc.am_re = (uint8_t)(pk2 >> 24);
-				oc.ref_l = (uint8_t)(pk3 & 1);
-				oc.ref_r = (uint8_t)((pk3 >> 1) & 1);
-				dsb_seedinfo_t os = {bin_read, w->L, (uint16_t)(pk3 >> 16), s_d->direction};
-				dsb_anchor_t an;
-				int pass = it < tot ? dsb_map_item(w, &oc, it - opfx, &os, &an) : 0;
-				uint64_t pm = dsb_wballot(pass);
-				uint32_t start = opfx > cb ? opfx - cb : 0; /* the owner's first item in this chunk */
-				uint64_t before = (lane == 0 ? 0 : (~0ull >> (64 - lane))) & ~(start == 0 ? 0 : (~0ull >> (64 - start)));
-				uint32_t dest = o_n + (uint32_t)__builtin_popcountll(pm & before);
-				if (pass && dest < S) {
-					w->anc_tmp[(uint64_t)o * S + dest] = an;
-					if (w->stats) w->stats[DSB_ST_ANCHOR]++;
-				}
-				/* owners: count their kept items of this chunk */
-				if (inmap) {
-					uint32_t lo = pfx > cb ? pfx - cb : 0, hi = DSB_MIN(pfx + cnt, cb + DSB_WV) - cb;
-					if (pfx + cnt > cb && lo < hi) {
-						uint64_t mine = (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & ~(lo == 0 ? 0ull : ((1ull << lo) - 1));
-						n_before += (uint32_t)__builtin_popcountll(pm & mine);
-					}
-				}
-			}
-			dsb_wsync();
-			if (inmap) {
-				int c_score = cx.ret;
-				if (cx.n_items) { /* max over the kept anchors (the reference's max_s) */
-					if (n_before > S) {
-						w->overflow |= 1;
-						n_before = S;
-					}
-					c_score = 0;
-					for (uint32_t a = w->n_anc; a < n_before; a++)
-						c_score = DSB_MAX(c_score, (int)stg[a].score);
-					w->n_anc = n_before;
-				}
-				if (w->stats) w->stats[DSB_ST_T_MAP] += dsb_clock() - t1;
-				max_score = DSB_MAX(c_score, max_score);
-				k_map++;
-			}
-		}
-		if (st == DSB_SM_MAP && do_map) {
-			if (k_map == n_m) {
-				if (w->overflow) {
-					st = DSB_SM_FIN;
-				} else {
-					if (max_score > 35)
-						j -= 7;
-					if (max_score > 256) {
-						if (max_score > 512)
-							skip = 1;
-						st = DSB_SM_FIN;
-					} else
-						st = DSB_SM_J;
-				}
-			}
-		}
-		/* ---- EXT / SS: one occ evaluation shared by both kinds of step */
-		if (st == DSB_SM_EXT || st == DSB_SM_SS) {
-			int ext = st == DSB_SM_EXT;
-			uint8_t c1 = ext ? *str : (uint8_t)0xff;
-			uint64_t o1 = dsb_occ_w(w, ext ? sp : ss_sp, &c1);
-			if (ext) {
-				uint8_t c2 = *str;
-				uint64_t o2 = dsb_occ_w(w, ep, &c2);
-				str--;
-				uint64_t new_sp = ix->rank[c1] + o1, new_ep = ix->rank[c2] + o2;
-				int done = 0, none = 0;
-				if (match_len >= DSB_MIN_MEM_LEN_FAST - 1 - 1) {
-					if (new_sp + DSB_MEM_SEARCH_FAST >= new_ep)
-						done = 1;
-					else if (match_len >= l_max)
-						none = 1;
-				}
-				if (!done && !none && new_sp + 1 >= new_ep)
-					done = 1;
-				if (none || (done && new_sp >= new_ep)) { /* no hit at this position */
-					n_m = 0;
-					j -= 2;
-					st = DSB_SM_J;
-				} else if (done) {
-					row = new_sp;
-					row_end = new_ep;
-					row_single = (new_sp + 1 == new_ep);
-					n_m = 0;
-					st = DSB_SM_ROW;
-				} else {
-					match_len++;
-					sp = new_sp;
-					ep = new_ep;
-				}
-			} else {
-				/* bwt_single_search: the symbol at ss_sp is c1, LF = o1 + rank */
-				uint64_t new_sp = o1 + ix->rank[c1];
-				int end = 0, dup = 0;
-				if (c1 != *ss_str) {
-					end = 1;
-				} else {
-					ss_len++;
-					ss_str--;
-					if (dsb_set_insert(new_sp, &hs) == 0)
-						dup = 1;
-					else
-						ss_sp = new_sp;
-				}
-				if (!end && !dup && ss_len >= ss_max)
-					end = 1;
-				if (!end && !dup) { /* SA-sample bookkeeping at the top of the next step */
-					if ((ss_sp & 7) == 0) {
-						sa_sp = ss_sp;
-						sa_sp_l = 0;
-					} else
-						sa_sp_l--;
-				} else {
-					dsb_mem_t *mr = m_r + n_m;
-					if (dup) {
-						mr->match_len = -1000;
-					} else {
-						mr->sp = ss_sp;
-						mr->match_len = ss_len;
-						mr->sa_sp = sa_sp;
-						mr->sa_sp_l = sa_sp_l;
-					}
-					mr->match_len += match_len + 1;
-					if (mr->match_len >= DSB_MIN_MEM_LEN_FAST - 1)
-						n_m++;
-					row++;
-					st = DSB_SM_ROW;
-				}
-			}
-		}
-		/* ---- ROW: rows of the final interval (sp_set), start single searches */
-		if (st == DSB_SM_ROW) {
-			for (;;) {
-				if (row >= row_end) {
-					if (n_m == 0) {
-						j -= 2;
-						st = DSB_SM_J;
-					} else {
-						j -= 3;
-						k_map = 0;
-						max_score = 0;
-						st = DSB_SM_MAP;
-					}
-					break;
-				}
-				if (dsb_set_insert(row, &hs) == 0) {
-					row = row_single ? row_end : row + 1;
-					continue;
-				}
-				ss_sp = row;
-				ss_str = str;
-				ss_max = DSB_MAX(0, l_max - match_len);
-				ss_len = 0;
-				sa_sp = ~0ull;
-				sa_sp_l = 0;
-				if (ss_max <= 0) { /* the single search ends before its first step */
-					dsb_mem_t *mr = m_r + n_m;
-					mr->sp = ss_sp;
-					mr->match_len = 0;
-					mr->sa_sp = sa_sp;
-					mr->sa_sp_l = sa_sp_l;
-					mr->match_len += match_len + 1;
-					if (mr->match_len >= DSB_MIN_MEM_LEN_FAST - 1)
-						n_m++;
-					row++;
-					continue;
-				}
-				if ((ss_sp & 7) == 0) {
-					sa_sp = ss_sp;
-					sa_sp_l = 0;
-				} else
-					sa_sp_l--;
-				st = DSB_SM_SS;
-				break;
-			}
-		}
-		/* ---- FIN: close the seed (anchors below its top score are useless) and record it */
-		if (st == DSB_SM_FIN) {
-			if (!w->overflow) {
-				int top_score = 35;
-				for (uint32_t a = a_b; a < w->n_anc; a++)
-					top_score = DSB_MAX(top_score, (int)stg[a].score);
-				for (uint32_t a = a_b; a < w->n_anc; a++)
-					stg[a].anchor_useless = (stg[a].score < top_score) ? 1 : 0;
-			}
-			rec[2 * k] = (lane << 24) | a_b;
-			rec[2 * k + 1] = ((uint32_t)(skip && !w->overflow) << 31) | ((uint32_t)(w->overflow != 0) << 30) |
-					 (w->overflow ? 0u : (w->n_anc - a_b));
-		}
-		/* ---- hand the next top seeds to the lanes that finished one, in lane order */
-		uint64_t finm = dsb_wballot(st == DSB_SM_FIN);
-		if (finm) {
-			uint64_t below = (lane == 0) ? 0 : (finm & (~0ull >> (64 - lane)));
-			uint32_t mine = next_k + (uint32_t)__builtin_popcountll(below);
-			next_k += (uint32_t)__builtin_popcountll(finm);
-			if (st == DSB_SM_FIN) {
-				if (w->overflow || mine >= m)
-					st = DSB_SM_DONE; /* an overflowed lane's staging is full: it retires */
-				else
-					DSB_SM_START_SEED(mine);
-			}
-		}
-		/* ---- J: start the FM search at position j of the seed */
-		if (st == DSB_SM_J) {
-			if (j < min_index) {
-				st = DSB_SM_FIN;
-			} else {
-				int kmer_index = (int)seed_off + j;
-				uint64_t kmer = dsb_kmer_at(bin_read + kmer_index, l_ek, ix->single_base_max);
-				uint64_t pre_v = kmer & DSB_PRE_IDX_MASK;
-				string_index = kmer_index + l_ek - 1;
-				if (w->stats) w->stats[DSB_ST_MEMSEARCH]++;
-				sp = ix->hash_index[pre_v];
-				ep = ix->hash_index[pre_v + 1];
-				str = bin_read + string_index - DSB_L_PRE_IDX;
-				match_len = DSB_L_PRE_IDX;
-				l_max = string_index;
-				n_m = 0;
-				st = DSB_SM_EXT;
-			}
-		}
-	}
-#undef DSB_SM_START_SEED
-	dsb_wsync();
-	w->anc = anc0;
-	w->n_anc = n0;
-	w->cap.anc = cap0;
-	w->overflow = of0;
-	/* ---- skip rule + ordered compaction over the seed records (as dsb_fast_classify_wave) */
-	int last_trig = 0;
-	uint32_t last_ci = 0;
-	for (uint32_t gb = 0; gb < m; gb += DSB_WV) {
-		uint32_t kk = gb + lane;
-		uint32_t gn = DSB_MIN((uint32_t)DSB_WV, m - gb);
-		int act = kk < m;
-		uint32_t cix = act ? tix[kk] : 0;
-		uint32_t r0 = act ? rec[2 * kk] : 0, r1 = act ? rec[2 * kk + 1] : 0;
-		int trig = (int)(r1 >> 31), ovf = (int)((r1 >> 30) & 1);
-		uint32_t cnt = r1 & 0x3fffffffu, src_lane = r0 >> 24, src_off = r0 & 0xffffffu;
-		uint64_t tm = dsb_wballot(act && trig);
-		uint64_t om = dsb_wballot(act && ovf);
-		uint64_t skipm = 0;
-		int lt = last_trig;
-		uint32_t lc = last_ci;
-		int unknown = 0;
-		for (uint32_t q = 0; q < gn; q++) {
-			uint32_t cq = (uint32_t)dsb_wshfl((int)cix, (int)q);
-			if (lt && cq == lc + 1) {
-				skipm |= 1ull << q;
-				lt = 0;
-				continue;
-			}
-			if ((om >> q) & 1)
-				unknown = 1;
-			lt = (int)((tm >> q) & 1);
-			lc = cq;
-		}
-		if (!unknown) {
-			last_trig = lt;
-			last_ci = lc;
-			if ((skipm >> lane) & 1)
-				cnt = 0;
-			uint32_t tot, off = dsb_wscan(cnt, &tot);
-			if (w->n_anc + tot > w->cap.anc) {
-				w->overflow |= 1;
-				dsb_wsync();
-				return;
-			}
-			const dsb_anchor_t *src = w->anc_tmp + (uint64_t)src_lane * S + src_off;
-			for (uint32_t e = 0; e < cnt; e++)
-				w->anc[w->n_anc + off + e] = src[e];
-			w->n_anc += tot;
-		} else { /* seed by seed, in order, deciding the skips as the reference does */
-			for (uint32_t q = 0; q < gn; q++) {
-				uint32_t cq = (uint32_t)dsb_wshfl((int)cix, (int)q);
-				if (last_trig && cq == last_ci + 1) {
-					last_trig = 0;
-					continue;
-				}
-				if ((om >> q) & 1) { /* replay on every lane, straight into the anchor vector */
-					last_trig = dsb_fast_seed(w, s_d, cq, &hs);
-					if (w->overflow) {
-						dsb_wsync();
-						return;
-					}
-				} else {
-					last_trig = (int)((tm >> q) & 1);
-					uint32_t kc = (uint32_t)dsb_wshfl((int)cnt, (int)q);
-					uint32_t sl = (uint32_t)dsb_wshfl((int)src_lane, (int)q), so = (uint32_t)dsb_wshfl((int)src_off, (int)q);
-					if (w->n_anc + kc > w->cap.anc) {
-						w->overflow |= 1;
-						dsb_wsync();
-						return;
-					}
-					const dsb_anchor_t *src = w->anc_tmp + (uint64_t)sl * S + so;
-					for (uint32_t e = lane; e < kc; e += DSB_WV)
-						w->anc[w->n_anc + e] = src[e];
-					w->n_anc += kc;
-				}
-				last_ci = cq;
-				dsb_wsync();
-			}
-		}
-		dsb_wsync();
-	}
-}
-
 #define DSB_MEM_SEARCH_SLOW 8
 #define DSB_MIN_MEM_LEN_SLOW 20
 /* One seed of slow_classify (src/cly.c:1556-1603): MEM searches every other position of the
@@ -1608,6 +1187,482 @@ DSB_HDN void dsb_slow_classify_wave(dsb_read_ws *w, const dsb_sdir_t *sd, uint64
 		dsb_wsync();
 	}
 	w->fast_classify = 0;
+}
+
+template <bool SLOW>
+DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, dsb_mem_t *memtmp)
+{
+	const dsb_dindex_t *ix = w->ix;
+	uint32_t lane = dsb_lane();
+	uint32_t n_sv = s_d->l_seed_v_f;
+	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV; /* dbg 32: tiny staging (tests the replay) */
+	dsb_anchor_t *stg = w->anc_tmp + (uint64_t)lane * S;
+	dsb_hset_t hs = {hset + lane, DSB_WV, 0, 0, 500};
+	uint8_t l_ek = (uint8_t)ix->l_ek;
+	int min_index = DSB_MIN_MEM_LEN_FAST - l_ek;
+	/* bwt_MEM_search parameters: fast src/cly.c:1500-1501, slow src/cly.c:1568-1570 */
+	const int MAX_RST = SLOW ? DSB_MEM_SEARCH_SLOW : DSB_MEM_SEARCH_FAST;
+	const int L_MIN = SLOW ? DSB_MIN(DSB_MIN_MEM_LEN_SLOW - 1, (int)l_ek + 1) : DSB_MIN_MEM_LEN_FAST - 1;
+	dsb_mem_t *top = memtmp + (uint64_t)lane * (2 * DSB_MEM_SEARCH_SLOW); /* slow: stable top-8 hits */
+	int n_top = 0, total = 0;
+	uint8_t *bin_read = w->bin + (s_d->strand ? w->L : 0);
+	/* ---- top seeds, in order (tix) */
+	uint32_t *tix = w->sidx, *rec = w->hh[0]; /* records: the read-hash region is free while seeding */
+	uint32_t m = 0;
+	for (uint32_t gb = 0; gb < n_sv; gb += DSB_WV) {
+		uint32_t ci = gb + lane;
+		int t = ci < n_sv && (SLOW ? dsb_slow_takes(w, s_d, ci) : w->seeds[s_d->seed_off + ci].top != 0);
+		uint64_t bm = dsb_wballot(t);
+		uint64_t below = (lane == 0) ? 0 : (bm & (~0ull >> (64 - lane)));
+		if (t)
+			tix[m + (uint32_t)__builtin_popcountll(below)] = ci;
+		m += (uint32_t)__builtin_popcountll(bm);
+	}
+	dsb_wsync();
+	if (m == 0) {
+		if (SLOW)
+			w->fast_classify = 0;
+		return;
+	}
+	/* ---- the lane's anchor vector is its staging area while seeds run */
+	dsb_anchor_t *anc0 = w->anc;
+	uint32_t n0 = w->n_anc, cap0 = w->cap.anc, of0 = w->overflow;
+	w->anc = stg;
+	w->n_anc = 0;
+	w->cap.anc = S;
+	w->overflow = 0;
+	/* ---- per-lane seed state; every record starts as "overflowed" (replayed if never written) */
+	for (uint32_t q = lane; q < m; q += DSB_WV) {
+		rec[2 * q] = 0;
+		rec[2 * q + 1] = 1u << 30;
+	}
+	dsb_wsync();
+	uint32_t next_k = DSB_MIN((uint32_t)DSB_WV, m); /* next top seed to hand out (uniform) */
+	uint32_t k = lane;                                /* my top-seed index */
+	int st = DSB_SM_DONE;
+	uint32_t ci = 0, a_b = 0, seed_off = 0;
+	int j = 0, skip = 0, n_m = 0, k_map = 0, max_score = 0, string_index = 0, match_len = 0, row_single = 0;
+	uint64_t sp = 0, ep = 0, row = 0, row_end = 0, ss_sp = 0, sa_sp = 0;
+	int ss_len = 0, ss_max = 0, sa_sp_l = 0, l_max = 0;
+	const uint8_t *str = bin_read, *ss_str = bin_read;
+	dsb_mem_t m_r[DSB_MEM_SEARCH_FAST];
+	for (int q = 0; q < DSB_MEM_SEARCH_FAST; q++) {
+		m_r[q].match_len = 0; m_r[q].sp = 0; m_r[q].sa_sp = 0; m_r[q].sa_sp_l = 0; m_r[q].kmer_index = 0; m_r[q].read_offset = 0;
+	}
+#define DSB_SM_START_SEED(K)                                                   \
+	do {                                                                   \
+		k = (K);                                                       \
+		ci = tix[k];                                                   \
+		const dsb_seed_t *c_sv_ = w->seeds + s_d->seed_off + ci;       \
+		seed_off = c_sv_->offset;                                      \
+		j = (int)c_sv_->len - 1;                                       \
+		skip = 0;                                                      \
+		n_top = 0;                                                     \
+		total = 0;                                                     \
+		a_b = w->n_anc;                                                \
+		dsb_set_reset(&hs);                                            \
+		st = DSB_SM_J;                                                 \
+	} while (0)
+	/* a finished single search: fast keeps hits >= L_MIN in m_r (src/cly.c:1424-1426); slow keeps a
+	 * stable top 8 by match length of all hits of the seed (the qsort of src/cly.c:1590) */
+#define DSB_SM_KEEP(R)                                                                         \
+	do {                                                                                   \
+		if ((R).match_len >= L_MIN) {                                                  \
+			if (!SLOW) {                                                           \
+				m_r[n_m] = (R);                                                \
+				n_m++;                                                         \
+			} else {                                                               \
+				(R).read_offset = string_index - (R).match_len;                \
+				total++;                                                       \
+				int p_ = 0;                                                    \
+				while (p_ < n_top && top[p_].match_len >= (R).match_len)       \
+					p_++;                                                  \
+				if (p_ < DSB_MEM_SEARCH_SLOW) {                                \
+					for (int q_ = DSB_MIN(n_top, DSB_MEM_SEARCH_SLOW - 1); q_ > p_; q_--) \
+						top[q_] = top[q_ - 1];                         \
+					top[p_] = (R);                                         \
+					n_top = DSB_MIN(n_top + 1, DSB_MEM_SEARCH_SLOW);       \
+				}                                                              \
+			}                                                                      \
+		}                                                                              \
+	} while (0)
+	if (k < m)
+		DSB_SM_START_SEED(lane);
+	for (;;) {
+		uint64_t act = dsb_wballot(st != DSB_SM_DONE);
+		if (!act)
+			break;
+		uint64_t mapm = dsb_wballot(st == DSB_SM_MAP);
+		int do_map = mapm != 0 && ((uint32_t)__builtin_popcountll(mapm) >= DSB_SM_MAP_BATCH || mapm == act);
+		/* ---- MAP: map_seed of hit k_map, batched; its REF_POS entries are spread over the wave.
+		 * Items are numbered owner by owner (lane order), REF_POS order inside an owner; a kept
+		 * Anchor goes to its owner's staging at the owner's count + the number of kept items of
+		 * that owner before it, i.e. the order of the reference's loop (src/cly.c:886-931). */
+		if (do_map) {
+			uint64_t t1 = w->stats ? dsb_clock() : 0;
+			int inmap = st == DSB_SM_MAP;
+			dsb_mapctx_t cx;
+			cx.n_items = 0;
+			cx.ret = 0;
+			dsb_seedinfo_t s_i = {bin_read, w->L, (uint16_t)ci, s_d->direction};
+			if (inmap) {
+				dsb_mem_t *mq = SLOW ? top + k_map : m_r + k_map;
+				if (!SLOW)
+					mq->read_offset = string_index - mq->match_len;
+				dsb_map_seed_pre(w, mq, &s_i, &cx);
+			}
+			uint32_t cnt = inmap ? cx.n_items : 0;
+			uint32_t tot, pfx = dsb_wscan(cnt, &tot);
+			uint32_t n_before = w->n_anc;
+			for (uint32_t cb = 0; cb < tot; cb += DSB_WV) {
+				uint32_t it = cb + lane;
+				int o = 0; /* owner: the last lane whose prefix is <= it */
+				for (int step = DSB_WV / 2; step > 0; step >>= 1)
+					if ((uint32_t)dsb_wshfl_any((int)pfx, o + step) <= it)
+						o += step;
+				dsb_mapctx_t oc;
+				uint32_t opfx = (uint32_t)dsb_wshfl_any((int)pfx, o);
+				oc.rp_s = ((uint64_t)(uint32_t)dsb_wshfl_any((int)(uint32_t)(cx.rp_s >> 32), o) << 32) |
+					  (uint32_t)dsb_wshfl_any((int)(uint32_t)cx.rp_s, o);
+				oc.q_off = dsb_wshfl_any(cx.q_off, o);
+				oc.l_m = (uint32_t)dsb_wshfl_any((int)cx.l_m, o);
+				oc.u_off = (uint32_t)dsb_wshfl_any((int)cx.u_off, o);
+				uint32_t pk1 = (uint32_t)cx.am_mtch | ((uint32_t)(uint16_t)cx.am_score << 16);
+				uint32_t pk2 = (uint32_t)cx.am_ll | ((uint32_t)cx.am_le << 8) | ((uint32_t)cx.am_rl << 16) |
+					       ((uint32_t)cx.am_re << 24);
+				uint32_t pk3 = (uint32_t)cx.ref_l | ((uint32_t)cx.ref_r << 1) | ((ci & 0xffffu) << 16);
+				pk1 = (uint32_t)dsb_wshfl_any((int)pk1, o);
+				pk2 = (uint32_t)dsb_wshfl_any((int)pk2, o);
+				pk3 = (uint32_t)dsb_wshfl_any((int)pk3, o);
+				uint32_t o_n = (uint32_t)dsb_wshfl_any((int)n_before, o);
+				oc.am_mtch = (uint16_t)pk1;
+				oc.am_score = (int16_t)(pk1 >> 16);
+				oc.am_ll = (uint8_t)pk2; oc.am_le = (uint8_t)(pk2 >> 8); oc.am_rl = (uint8_t)(pk2 >> 16);
+				oc.am_re = (uint8_t)(pk2 >> 24);
+				oc.ref_l = (uint8_t)(pk3 & 1);
+				oc.ref_r = (uint8_t)((pk3 >> 1) & 1);
+				dsb_seedinfo_t os = {bin_read, w->L, (uint16_t)(pk3 >> 16), s_d->direction};
+				dsb_anchor_t an;
+				int pass = it < tot ? dsb_map_item(w, &oc, it - opfx, &os, &an) : 0;
+				uint64_t pm = dsb_wballot(pass);
+				uint32_t start = opfx > cb ? opfx - cb : 0; /* the owner's first item in this chunk */
+				uint64_t before = (lane == 0 ? 0 : (~0ull >> (64 - lane))) & ~(start == 0 ? 0 : (~0ull >> (64 - start)));
+				uint32_t dest = o_n + (uint32_t)__builtin_popcountll(pm & before);
+				if (pass && dest < S) {
+					w->anc_tmp[(uint64_t)o * S + dest] = an;
+					if (w->stats) w->stats[DSB_ST_ANCHOR]++;
+				}
+				/* owners: count their kept items of this chunk */
+				if (inmap) {
+					uint32_t lo = pfx > cb ? pfx - cb : 0, hi = DSB_MIN(pfx + cnt, cb + DSB_WV) - cb;
+					if (pfx + cnt > cb && lo < hi) {
+						uint64_t mine = (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & ~(lo == 0 ? 0ull : ((1ull << lo) - 1));
+						n_before += (uint32_t)__builtin_popcountll(pm & mine);
+					}
+				}
+			}
+			dsb_wsync();
+			if (inmap) {
+				int c_score = cx.ret;
+				if (cx.n_items) { /* max over the kept anchors (the reference's max_s) */
+					if (n_before > S) {
+						w->overflow |= 1;
+						n_before = S;
+					}
+					c_score = 0;
+					for (uint32_t a = w->n_anc; a < n_before; a++)
+						c_score = DSB_MAX(c_score, (int)stg[a].score);
+					w->n_anc = n_before;
+				}
+				if (w->stats) w->stats[DSB_ST_T_MAP] += dsb_clock() - t1;
+				max_score = DSB_MAX(c_score, max_score);
+				k_map++;
+			}
+		}
+		if (st == DSB_SM_MAP && do_map) {
+			if (k_map == n_m) {
+				if (SLOW || w->overflow) {
+					st = DSB_SM_FIN;
+				} else {
+					if (max_score > 35)
+						j -= 7;
+					if (max_score > 256) {
+						if (max_score > 512)
+							skip = 1;
+						st = DSB_SM_FIN;
+					} else
+						st = DSB_SM_J;
+				}
+			}
+		}
+		/* ---- EXT / SS: one occ evaluation shared by both kinds of step */
+		if (st == DSB_SM_EXT || st == DSB_SM_SS) {
+			int ext = st == DSB_SM_EXT;
+			uint8_t c1 = ext ? *str : (uint8_t)0xff;
+			uint64_t o1 = dsb_occ_w(w, ext ? sp : ss_sp, &c1);
+			if (ext) {
+				uint8_t c2 = *str;
+				uint64_t o2 = dsb_occ_w(w, ep, &c2);
+				str--;
+				uint64_t new_sp = ix->rank[c1] + o1, new_ep = ix->rank[c2] + o2;
+				int done = 0, none = 0;
+				if (match_len >= L_MIN - 1) {
+					if (new_sp + (uint64_t)MAX_RST >= new_ep)
+						done = 1;
+					else if (match_len >= l_max)
+						none = 1;
+				}
+				if (!done && !none && new_sp + 1 >= new_ep)
+					done = 1;
+				if (none || (done && new_sp >= new_ep)) { /* no hit at this position */
+					n_m = 0;
+					j -= 2;
+					st = DSB_SM_J;
+				} else if (done) {
+					row = new_sp;
+					row_end = new_ep;
+					row_single = (new_sp + 1 == new_ep);
+					n_m = 0;
+					st = DSB_SM_ROW;
+				} else {
+					match_len++;
+					sp = new_sp;
+					ep = new_ep;
+				}
+			} else {
+				/* bwt_single_search: the symbol at ss_sp is c1, LF = o1 + rank */
+				uint64_t new_sp = o1 + ix->rank[c1];
+				int end = 0, dup = 0;
+				if (c1 != *ss_str) {
+					end = 1;
+				} else {
+					ss_len++;
+					ss_str--;
+					if (dsb_set_insert(new_sp, &hs) == 0)
+						dup = 1;
+					else
+						ss_sp = new_sp;
+				}
+				if (!end && !dup && ss_len >= ss_max)
+					end = 1;
+				if (!end && !dup) { /* SA-sample bookkeeping at the top of the next step */
+					if ((ss_sp & 7) == 0) {
+						sa_sp = ss_sp;
+						sa_sp_l = 0;
+					} else
+						sa_sp_l--;
+				} else {
+					dsb_mem_t r;
+					r.kmer_index = 0;
+					r.read_offset = 0;
+					r.sp = ss_sp;
+					r.match_len = dup ? -1000 : ss_len;
+					r.sa_sp = sa_sp;
+					r.sa_sp_l = sa_sp_l;
+					r.match_len += match_len + 1;
+					DSB_SM_KEEP(r);
+					row++;
+					st = DSB_SM_ROW;
+				}
+			}
+		}
+		/* ---- ROW: rows of the final interval (sp_set), start single searches */
+		if (st == DSB_SM_ROW) {
+			for (;;) {
+				if (row >= row_end) {
+					if (SLOW || n_m == 0) {
+						j -= 2;
+						st = DSB_SM_J;
+					} else {
+						j -= 3;
+						k_map = 0;
+						max_score = 0;
+						st = DSB_SM_MAP;
+					}
+					break;
+				}
+				if (dsb_set_insert(row, &hs) == 0) {
+					row = row_single ? row_end : row + 1;
+					continue;
+				}
+				ss_sp = row;
+				ss_str = str;
+				ss_max = DSB_MAX(0, l_max - match_len);
+				ss_len = 0;
+				sa_sp = ~0ull;
+				sa_sp_l = 0;
+				if (ss_max <= 0) { /* the single search ends before its first step */
+					dsb_mem_t r;
+					r.kmer_index = 0;
+					r.read_offset = 0;
+					r.sp = ss_sp;
+					r.match_len = match_len + 1;
+					r.sa_sp = sa_sp;
+					r.sa_sp_l = sa_sp_l;
+					DSB_SM_KEEP(r);
+					row++;
+					continue;
+				}
+				if ((ss_sp & 7) == 0) {
+					sa_sp = ss_sp;
+					sa_sp_l = 0;
+				} else
+					sa_sp_l--;
+				st = DSB_SM_SS;
+				break;
+			}
+		}
+		/* ---- FIN: close the seed (anchors below its top score are useless) and record it */
+		if (st == DSB_SM_FIN) {
+			if (!w->overflow) {
+				int top_score = 35;
+				for (uint32_t a = a_b; a < w->n_anc; a++)
+					top_score = DSB_MAX(top_score, (int)stg[a].score);
+				for (uint32_t a = a_b; a < w->n_anc; a++)
+					stg[a].anchor_useless = (stg[a].score < top_score) ? 1 : 0;
+			}
+			rec[2 * k] = (lane << 24) | a_b;
+			rec[2 * k + 1] = ((uint32_t)(!SLOW && skip && !w->overflow) << 31) | ((uint32_t)(w->overflow != 0) << 30) |
+					 (w->overflow ? 0u : (w->n_anc - a_b));
+		}
+		/* ---- hand the next top seeds to the lanes that finished one, in lane order */
+		uint64_t finm = dsb_wballot(st == DSB_SM_FIN);
+		if (finm) {
+			uint64_t below = (lane == 0) ? 0 : (finm & (~0ull >> (64 - lane)));
+			uint32_t mine = next_k + (uint32_t)__builtin_popcountll(below);
+			next_k += (uint32_t)__builtin_popcountll(finm);
+			if (st == DSB_SM_FIN) {
+				if (w->overflow || mine >= m)
+					st = DSB_SM_DONE; /* an overflowed lane's staging is full: it retires */
+				else
+					DSB_SM_START_SEED(mine);
+			}
+		}
+		/* ---- J: start the FM search at position j of the seed */
+		if (st == DSB_SM_J) {
+			if (SLOW ? j < 1 : j < min_index) {
+				if (SLOW && total > 0) { /* map the kept top hits (src/cly.c:1590-1597) */
+					n_m = n_top;
+					k_map = 0;
+					st = DSB_SM_MAP;
+				} else
+					st = DSB_SM_FIN;
+			} else {
+				int kmer_index = (int)seed_off + j;
+				uint64_t kmer = dsb_kmer_at(bin_read + kmer_index, l_ek, ix->single_base_max);
+				uint64_t pre_v = kmer & DSB_PRE_IDX_MASK;
+				string_index = kmer_index + l_ek - 1;
+				if (w->stats) w->stats[DSB_ST_MEMSEARCH]++;
+				sp = ix->hash_index[pre_v];
+				ep = ix->hash_index[pre_v + 1];
+				str = bin_read + string_index - DSB_L_PRE_IDX;
+				match_len = DSB_L_PRE_IDX;
+				l_max = string_index;
+				n_m = 0;
+				st = DSB_SM_EXT;
+			}
+		}
+	}
+#undef DSB_SM_START_SEED
+#undef DSB_SM_KEEP
+	dsb_wsync();
+	w->anc = anc0;
+	w->n_anc = n0;
+	w->cap.anc = cap0;
+	w->overflow = of0;
+	/* ---- skip rule + ordered compaction over the seed records (as dsb_fast_classify_wave) */
+	int last_trig = 0;
+	uint32_t last_ci = 0;
+	for (uint32_t gb = 0; gb < m; gb += DSB_WV) {
+		uint32_t kk = gb + lane;
+		uint32_t gn = DSB_MIN((uint32_t)DSB_WV, m - gb);
+		int act = kk < m;
+		uint32_t cix = act ? tix[kk] : 0;
+		uint32_t r0 = act ? rec[2 * kk] : 0, r1 = act ? rec[2 * kk + 1] : 0;
+		int trig = (int)(r1 >> 31), ovf = (int)((r1 >> 30) & 1);
+		uint32_t cnt = r1 & 0x3fffffffu, src_lane = r0 >> 24, src_off = r0 & 0xffffffu;
+		uint64_t tm = dsb_wballot(act && trig);
+		uint64_t om = dsb_wballot(act && ovf);
+		uint64_t skipm = 0;
+		int lt = last_trig;
+		uint32_t lc = last_ci;
+		int unknown = 0;
+		for (uint32_t q = 0; q < gn; q++) {
+			uint32_t cq = (uint32_t)dsb_wshfl((int)cix, (int)q);
+			if (lt && cq == lc + 1) {
+				skipm |= 1ull << q;
+				lt = 0;
+				continue;
+			}
+			if ((om >> q) & 1)
+				unknown = 1;
+			lt = (int)((tm >> q) & 1);
+			lc = cq;
+		}
+		if (!unknown) {
+			last_trig = lt;
+			last_ci = lc;
+			if ((skipm >> lane) & 1)
+				cnt = 0;
+			uint32_t tot, off = dsb_wscan(cnt, &tot);
+			if (w->n_anc + tot > w->cap.anc) {
+				w->overflow |= 1;
+				dsb_wsync();
+				return;
+			}
+			const dsb_anchor_t *src = w->anc_tmp + (uint64_t)src_lane * S + src_off;
+			for (uint32_t e = 0; e < cnt; e++)
+				w->anc[w->n_anc + off + e] = src[e];
+			w->n_anc += tot;
+		} else { /* seed by seed, in order, deciding the skips as the reference does */
+			for (uint32_t q = 0; q < gn; q++) {
+				uint32_t cq = (uint32_t)dsb_wshfl((int)cix, (int)q);
+				if (last_trig && cq == last_ci + 1) {
+					last_trig = 0;
+					continue;
+				}
+				if ((om >> q) & 1) { /* replay on every lane, straight into the anchor vector */
+					if (SLOW) {
+						dsb_slow_seed(w, s_d, cq, &hs, top);
+						last_trig = 0;
+					} else
+						last_trig = dsb_fast_seed(w, s_d, cq, &hs);
+					if (w->overflow) {
+						dsb_wsync();
+						return;
+					}
+				} else {
+					last_trig = (int)((tm >> q) & 1);
+					uint32_t kc = (uint32_t)dsb_wshfl((int)cnt, (int)q);
+					uint32_t sl = (uint32_t)dsb_wshfl((int)src_lane, (int)q), so = (uint32_t)dsb_wshfl((int)src_off, (int)q);
+					if (w->n_anc + kc > w->cap.anc) {
+						w->overflow |= 1;
+						dsb_wsync();
+						return;
+					}
+					const dsb_anchor_t *src = w->anc_tmp + (uint64_t)sl * S + so;
+					for (uint32_t e = lane; e < kc; e += DSB_WV)
+						w->anc[w->n_anc + e] = src[e];
+					w->n_anc += kc;
+				}
+				last_ci = cq;
+				dsb_wsync();
+			}
+		}
+		dsb_wsync();
+	}
+	if (SLOW)
+		w->fast_classify = 0;
+}
+
+/* fast_classify / slow_classify with one wavefront per read: the per-lane state machine */
+DSB_HDN void dsb_fast_classify_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset)
+{
+	dsb_seed_sm<false>(w, s_d, hset, w->mem);
+}
+DSB_HDN void dsb_slow_classify_sm(dsb_read_ws *w, const dsb_sdir_t *sd, uint64_t *hset, dsb_mem_t *memtmp)
+{
+	dsb_seed_sm<true>(w, sd, hset, memtmp);
 }
 
 /* ------------------------------------------------------------------ chaining */

@@ -128,7 +128,7 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
 				hset[k] = 0;
 			__syncthreads();
-			dsb_slow_classify_wave(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem);
+			dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem);
 		} else
 			dsb_phase<true>(&w, &f, ph);
 	}

@@ -109,7 +109,7 @@ int main(int argc, char **argv)
 						dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset);
 					} else if ((ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) && dsb_phase_active(&w, &f, ph)) {
 						memset(hset, 0, 8ull * DSB_HSET_SLOTS * 64);
-						dsb_slow_classify_wave(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem);
+						dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem);
 					} else
 						dsb_phase<true>(&w, &f, ph);
 				}
