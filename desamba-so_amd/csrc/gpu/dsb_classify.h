@@ -896,133 +896,11 @@ DSB_HDN void dsb_fast_classify(dsb_read_ws *w, const dsb_sdir_t *s_d)
 }
 
 /*
- * fast_classify with one wavefront per read.  Only `top` seeds do work, so their indices are
- * first compacted (ballot + prefix, in seed order) and handed out 64 at a time, one per lane.
- * Each lane runs its seed into a private staging area (anc_tmp, S anchors per lane) with its
- * own hashed sp_set.  The reference's `ci++` (src/cly.c:1526: after a seed scoring > 512 the
- * next seed index is skipped) is replayed in order over the group: a top seed is skipped iff
- * the previously processed seed triggered and sits immediately before it.  Kept anchors are
- * compacted into the anchor vector in seed order (prefix sum).  A group in which some lane
- * overflowed its staging area is replayed seed by seed in order.  hset: DSB_HSET_SLOTS x
- * DSB_WV slots, lane-interleaved, zeroed by the caller; the top list lives in w->sidx.
- */
-DSB_HDN void dsb_fast_classify_wave(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset)
-{
-	uint32_t lane = dsb_lane();
-	uint32_t n_sv = s_d->l_seed_v_f;
-	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV; /* dbg 32: tiny staging (tests the replay) */
-	dsb_anchor_t *stg = w->anc_tmp + (uint64_t)lane * S;
-	dsb_hset_t hs = {hset + lane, DSB_WV, 0, 0, 500};
-	/* ---- top seeds, in order */
-	uint32_t *tix = w->sidx;
-	uint32_t m = 0;
-	for (uint32_t gb = 0; gb < n_sv; gb += DSB_WV) {
-		uint32_t ci = gb + lane;
-		int t = ci < n_sv && w->seeds[s_d->seed_off + ci].top != 0;
-		uint64_t bm = dsb_wballot(t);
-		uint64_t below = (lane == 0) ? 0 : (bm & (~0ull >> (64 - lane)));
-		if (t)
-			tix[m + (uint32_t)__builtin_popcountll(below)] = ci;
-		m += (uint32_t)__builtin_popcountll(bm);
-	}
-	dsb_wsync();
-	int last_trig = 0;     /* the previously processed seed triggered the skip */
-	uint32_t last_ci = 0;  /* ... and its index */
-	for (uint32_t gb = 0; gb < m; gb += DSB_WV) {
-		uint32_t k = gb + lane;
-		uint32_t gn = DSB_MIN((uint32_t)DSB_WV, m - gb);
-		int act = k < m;
-		uint32_t ci = act ? tix[k] : 0;
-		int trig = 0, ovf = 0;
-		uint32_t cnt = 0;
-		if (act) {
-			dsb_anchor_t *anc0 = w->anc;
-			uint32_t n0 = w->n_anc, cap0 = w->cap.anc, of0 = w->overflow;
-			w->anc = stg;
-			w->n_anc = 0;
-			w->cap.anc = S;
-			w->overflow = 0;
-			trig = dsb_fast_seed(w, s_d, ci, &hs);
-			cnt = w->n_anc;
-			ovf = w->overflow != 0;
-			w->anc = anc0;
-			w->n_anc = n0;
-			w->cap.anc = cap0;
-			w->overflow = of0;
-		}
-		uint64_t tm = dsb_wballot(act && trig);
-		uint64_t om = dsb_wballot(act && ovf); /* an overflowed lane's trigger is not known yet */
-		/* skips over the group in order (lanes' seed indices via shuffles) */
-		uint64_t skipm = 0;
-		int lt = last_trig;
-		uint32_t lc = last_ci;
-		int unknown = 0;
-		for (uint32_t q = 0; q < gn; q++) {
-			uint32_t cq = (uint32_t)dsb_wshfl((int)ci, (int)q);
-			if (lt && cq == lc + 1) {
-				skipm |= 1ull << q;
-				lt = 0;
-				continue;
-			}
-			if ((om >> q) & 1)
-				unknown = 1;
-			lt = (int)((tm >> q) & 1);
-			lc = cq;
-		}
-		if (!unknown) {
-			last_trig = lt;
-			last_ci = lc;
-			if ((skipm >> lane) & 1)
-				cnt = 0;
-			uint32_t tot, off = dsb_wscan(cnt, &tot);
-			if (w->n_anc + tot > w->cap.anc) {
-				w->overflow |= 1;
-				dsb_wsync();
-				return;
-			}
-			for (uint32_t e = 0; e < cnt; e++)
-				w->anc[w->n_anc + off + e] = stg[e];
-			w->n_anc += tot;
-		} else { /* seed by seed, in order, deciding the skips as the reference does */
-			for (uint32_t q = 0; q < gn; q++) {
-				uint32_t cq = (uint32_t)dsb_wshfl((int)ci, (int)q);
-				if (last_trig && cq == last_ci + 1) {
-					last_trig = 0;
-					continue;
-				}
-				if ((om >> q) & 1) { /* replay on every lane, straight into the anchor vector */
-					last_trig = dsb_fast_seed(w, s_d, cq, &hs);
-					if (w->overflow) {
-						dsb_wsync();
-						return;
-					}
-				} else {
-					last_trig = (int)((tm >> q) & 1);
-					uint32_t kc = (uint32_t)dsb_wshfl((int)cnt, (int)q);
-					if (w->n_anc + kc > w->cap.anc) {
-						w->overflow |= 1;
-						dsb_wsync();
-						return;
-					}
-					const dsb_anchor_t *src = w->anc_tmp + (uint64_t)q * S;
-					for (uint32_t e = lane; e < kc; e += DSB_WV)
-						w->anc[w->n_anc + e] = src[e];
-					w->n_anc += kc;
-				}
-				last_ci = cq;
-				dsb_wsync();
-			}
-		}
-		dsb_wsync();
-	}
-}
-
-/*
  * fast_classify as a per-lane state machine (one wavefront per read).
  *
- * The straightforward lane-per-seed form (dsb_fast_classify_wave) runs each lane's nested loops
- * (FM extension, single-row extension, map_seed) in its own control flow: the lanes of a wave
- * diverge and the wave serialises them (measured VALU lane utilisation ~8 %).  Here every lane
+ * A lane-per-seed form (one seed per lane, each lane running the reference's nested loops in
+ * its own control flow) leaves the lanes of a wave diverged and the wave serialises them
+ * (measured VALU lane utilisation ~8 %).  Here every lane
  * advances its seed by one step per trip of a single wave-wide loop, so lanes doing the same
  * kind of step run together:
  *   J    start the next FM search at position j of the seed (k-mer, 13-mer prefix interval)
@@ -1036,7 +914,11 @@ DSB_HDN void dsb_fast_classify_wave(dsb_read_ws *w, const dsb_sdir_t *s_d, uint6
  * together.  Seeds are handed out in top-seed order as lanes become free; each seed's anchors
  * are staged in its lane's area and described by a record (lane, offset, count, trigger,
  * overflow), after which the reference's skip rule and the ordered compaction run over the
- * records exactly as in dsb_fast_classify_wave.
+ * records: a top seed is skipped iff the previously processed seed triggered the reference's
+ * `ci++` (src/cly.c:1526, score > 512) and sits immediately before it; kept anchors are
+ * compacted in seed order (prefix sum); a group holding an overflowed seed is replayed seed by
+ * seed in order.  SLOW (slow_classify, src/cly.c:1545-1606): every seed the reference takes,
+ * every 2nd k-mer, up to 8 rows per FM hit, the seed's stable top-8 hits mapped at its end.
  */
 #ifndef DSB_SM_MAP_BATCH
 #define DSB_SM_MAP_BATCH 64
@@ -1112,79 +994,6 @@ DSB_HDN void dsb_slow_classify(dsb_read_ws *w, const dsb_sdir_t *sd)
 		dsb_slow_seed(w, sd, i, &sp_set, w->mem);
 		if (w->overflow)
 			return;
-	}
-	w->fast_classify = 0;
-}
-
-/* slow_classify with one wavefront per read, seeds across lanes (as dsb_fast_classify_wave,
- * without the skip rule).  memtmp: 16 MEM results per lane. */
-DSB_HDN void dsb_slow_classify_wave(dsb_read_ws *w, const dsb_sdir_t *sd, uint64_t *hset, dsb_mem_t *memtmp)
-{
-	uint32_t lane = dsb_lane();
-	uint32_t n_sv = sd->l_seed_v_f;
-	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV;
-	dsb_anchor_t *stg = w->anc_tmp + (uint64_t)lane * S;
-	dsb_hset_t hs = {hset + lane, DSB_WV, 0, 0, 500};
-	dsb_mem_t *mt = memtmp + (uint64_t)lane * (2 * DSB_MEM_SEARCH_SLOW);
-	for (uint32_t gb = 0; gb < n_sv; gb += DSB_WV) {
-		uint32_t ci = gb + lane;
-		uint32_t gn = DSB_MIN((uint32_t)DSB_WV, n_sv - gb);
-		int act = ci < n_sv && dsb_slow_takes(w, sd, ci);
-		int ovf = 0;
-		uint32_t cnt = 0;
-		if (act) {
-			dsb_anchor_t *anc0 = w->anc;
-			uint32_t n0 = w->n_anc, cap0 = w->cap.anc, of0 = w->overflow;
-			w->anc = stg;
-			w->n_anc = 0;
-			w->cap.anc = S;
-			w->overflow = 0;
-			dsb_slow_seed(w, sd, ci, &hs, mt);
-			cnt = w->n_anc;
-			ovf = w->overflow != 0;
-			w->anc = anc0;
-			w->n_anc = n0;
-			w->cap.anc = cap0;
-			w->overflow = of0;
-		}
-		uint64_t om = dsb_wballot(act && ovf);
-		if (om == 0) {
-			uint32_t tot, off = dsb_wscan(cnt, &tot);
-			if (w->n_anc + tot > w->cap.anc) {
-				w->overflow |= 1;
-				dsb_wsync();
-				return;
-			}
-			for (uint32_t k = 0; k < cnt; k++)
-				w->anc[w->n_anc + off + k] = stg[k];
-			w->n_anc += tot;
-		} else {
-			for (uint32_t k = 0; k < gn; k++) {
-				uint32_t ck = gb + k;
-				if (!dsb_slow_takes(w, sd, ck))
-					continue;
-				if ((om >> k) & 1) {
-					dsb_slow_seed(w, sd, ck, &hs, mt);
-					if (w->overflow) {
-						dsb_wsync();
-						return;
-					}
-				} else {
-					uint32_t kc = (uint32_t)dsb_wshfl((int)cnt, (int)k);
-					if (w->n_anc + kc > w->cap.anc) {
-						w->overflow |= 1;
-						dsb_wsync();
-						return;
-					}
-					const dsb_anchor_t *src = w->anc_tmp + (uint64_t)k * S;
-					for (uint32_t e = lane; e < kc; e += DSB_WV)
-						w->anc[w->n_anc + e] = src[e];
-					w->n_anc += kc;
-				}
-				dsb_wsync();
-			}
-		}
-		dsb_wsync();
 	}
 	w->fast_classify = 0;
 }
@@ -1570,7 +1379,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	w->n_anc = n0;
 	w->cap.anc = cap0;
 	w->overflow = of0;
-	/* ---- skip rule + ordered compaction over the seed records (as dsb_fast_classify_wave) */
+	/* ---- skip rule + ordered compaction over the seed records */
 	int last_trig = 0;
 	uint32_t last_ci = 0;
 	for (uint32_t gb = 0; gb < m; gb += DSB_WV) {
