@@ -123,8 +123,8 @@ enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, 
        DSB_ST_HASH_B,   /* read 9-mer hash: bytes written/read while building it */
        DSB_ST_LOOKUP,   /* reference-window k-mer lookups into that hash (4 B head each) */
        DSB_ST_NODE,     /* hash-list nodes visited by those lookups (8 B each) */
-       DSB_ST_T_MEM,    /* shader clocks inside bwt_MEM_search (stats kernels only) */
-       DSB_ST_T_MAP,    /* shader clocks inside map_seed (stats kernels only) */
+       DSB_ST_T_MEM,    /* seeding: wave clocks of the seed state machine (stats kernels, lane 0) */
+       DSB_ST_T_MAP,    /* seeding: wave clocks of its batched map_seed steps (stats kernels, lane 0) */
        /* scoring phase clocks (stats kernels, lane 0) */
        DSB_ST_T_BUILD,  /* build_hash_table_M2 */
        DSB_ST_T_MATCH,  /* sdp_match */
@@ -587,7 +587,7 @@ DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t
 		dsb_copy32(qbuf, q - 8);
 		q = qbuf + 8;
 	}
-	*e_d = dsb_lv_extd(t, len, q, len);
+	*e_d = dsb_lv_extd_w(t, len, q, len);
 	*len_ = len;
 }
 
@@ -677,7 +677,7 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 			l_pre = DSB_MIN(l_pre, u_off);
 			dsb_get_ref_w(w, t_pre, t_off - 1, l_pre, 0);
 		}
-		d_pre = dsb_lv_extd(t_pre, l_pre, q_pre, l_pre);
+		d_pre = dsb_lv_extd_w(t_pre, l_pre, q_pre, l_pre);
 		s = dsb_qmem(ix, l_m) + Q_LV[d_pre * DSB_LV_DIM + l_pre];
 		if (s < DSB_MIN_S_1 && l_pre == DSB_LV_L && uni < 0) {
 			s = 0;
@@ -719,7 +719,7 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 			}
 			uint8_t qsuf_b[32]; /* private copy: lv_extd writes its terminator at q_suf[l_suf] */
 			dsb_copy32(qsuf_b, q_suf - 8);
-			d_suf = dsb_lv_extd(t_suf, l_suf, qsuf_b + 8, l_suf);
+			d_suf = dsb_lv_extd_w(t_suf, l_suf, qsuf_b + 8, l_suf);
 			s += Q_LV[d_suf * DSB_LV_DIM + l_suf];
 		} else
 			l_suf = d_suf = 0;
@@ -1097,6 +1097,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	} while (0)
 	if (k < m)
 		DSB_SM_START_SEED(lane);
+	uint64_t t_sm = DSB_T0();
 	for (;;) {
 		uint64_t act = dsb_wballot(st != DSB_SM_DONE);
 		if (!act)
@@ -1108,18 +1109,20 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 		 * Anchor goes to its owner's staging at the owner's count + the number of kept items of
 		 * that owner before it, i.e. the order of the reference's loop (src/cly.c:886-931). */
 		if (do_map) {
-			uint64_t t1 = w->stats ? dsb_clock() : 0;
+			uint64_t t1 = DSB_T0();
 			int inmap = st == DSB_SM_MAP;
 			dsb_mapctx_t cx;
 			cx.n_items = 0;
 			cx.ret = 0;
 			dsb_seedinfo_t s_i = {bin_read, w->L, (uint16_t)ci, s_d->direction};
+			uint64_t tp0 = DSB_T0();
 			if (inmap) {
 				dsb_mem_t *mq = SLOW ? top + k_map : m_r + k_map;
 				if (!SLOW)
 					mq->read_offset = string_index - mq->match_len;
 				dsb_map_seed_pre(w, mq, &s_i, &cx);
 			}
+			DSB_T1(DSB_ST_T_BUILD, tp0); /* lane 0: wave clocks in map_seed's prefix / suffix part */
 			uint32_t cnt = inmap ? cx.n_items : 0;
 			uint32_t tot, pfx = dsb_wscan(cnt, &tot);
 			uint32_t n_before = w->n_anc;
@@ -1183,10 +1186,10 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 						c_score = DSB_MAX(c_score, (int)stg[a].score);
 					w->n_anc = n_before;
 				}
-				if (w->stats) w->stats[DSB_ST_T_MAP] += dsb_clock() - t1;
 				max_score = DSB_MAX(c_score, max_score);
 				k_map++;
 			}
+			DSB_T1(DSB_ST_T_MAP, t1); /* lane 0: wave clocks in the batched map steps */
 		}
 		if (st == DSB_SM_MAP && do_map) {
 			if (k_map == n_m) {
@@ -1372,6 +1375,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 			}
 		}
 	}
+	DSB_T1(DSB_ST_T_MEM, t_sm); /* lane 0: wave clocks in the whole state machine */
 #undef DSB_SM_START_SEED
 #undef DSB_SM_KEEP
 	dsb_wsync();

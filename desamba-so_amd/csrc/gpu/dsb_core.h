@@ -391,6 +391,139 @@ DSB_HD int32_t dsb_lv_extd(uint8_t *ref, int32_t ref_length, uint8_t *query, int
 	return best_score;
 }
 
+/*
+ * lv_extd on a 32-byte window held in registers: ref / query point 8 bytes into 32-byte buffers
+ * (every caller's buffer), so the bytes the reference can touch, ref[-5 .. len+4]
+ * and query[-1 .. len], are four u64 words each.  The terminators go into the register copies
+ * (the caller's buffers are left as they are, as the reference restores them), and the in-line
+ * match `for (; ref[mn + j] == query[mn]; mn++)` compares 8 bytes per step (first differing byte
+ * of the XOR).  It always stops at query's '$' (ref holds no '$'), within the window.
+ * Same result as dsb_lv_extd for every input of that shape (tests/test_lv_words.py).
+ */
+DSB_HD uint64_t dsb_win8(const uint64_t *W, int x) /* bytes x .. x+7 of the window, x in [-8, 16] */
+{
+	int b = x + 8;
+	int i = b >> 3, sh = (b & 7) * 8;
+	uint64_t lo = W[0], hi = W[1];
+	if (i == 1) { lo = W[1]; hi = W[2]; }
+	if (i == 2) { lo = W[2]; hi = W[3]; }
+	if (i >= 3) { lo = W[3]; hi = 0; }
+	return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+}
+DSB_HD uint32_t dsb_byte_at(const uint64_t *W, int x)
+{
+	int b = x + 8;
+	uint64_t w0 = W[0];
+	if ((b >> 3) == 1) w0 = W[1];
+	if ((b >> 3) == 2) w0 = W[2];
+	if ((b >> 3) >= 3) w0 = W[3];
+	return (uint32_t)(w0 >> ((b & 7) * 8)) & 0xff;
+}
+DSB_HD void dsb_set_byte(uint64_t *W, int x, uint32_t v)
+{
+	int b = x + 8;
+	uint64_t m = 0xffull << ((b & 7) * 8), val = (uint64_t)v << ((b & 7) * 8);
+	int i = b >> 3;
+	if (i == 0) W[0] = (W[0] & ~m) | val;
+	if (i == 1) W[1] = (W[1] & ~m) | val;
+	if (i == 2) W[2] = (W[2] & ~m) | val;
+	if (i == 3) W[3] = (W[3] & ~m) | val;
+}
+DSB_HD int32_t dsb_lv_extd_w(const uint8_t *ref_, int32_t ref_length, const uint8_t *query_, int32_t query_length)
+{
+	uint64_t R[4], Q[4];
+	for (int k = 0; k < 4; k++) {
+		uint64_t a = 0, b = 0;
+		for (int e = 0; e < 8; e++) {
+			a |= (uint64_t)ref_[8 * k + e - 8] << (8 * e);
+			b |= (uint64_t)query_[8 * k + e - 8] << (8 * e);
+		}
+		R[k] = a;
+		Q[k] = b;
+	}
+	if (ref_length < query_length) {
+		int32_t t = ref_length; ref_length = query_length; query_length = t;
+		for (int k = 0; k < 4; k++) { uint64_t x = R[k]; R[k] = Q[k]; Q[k] = x; }
+	}
+	dsb_set_byte(R, ref_length, '#');
+	dsb_set_byte(Q, query_length, '$');
+	int32_t mnd[2 * DSB_LV_ERROR + 5], edd[2 * DSB_LV_ERROR + 5];
+	int32_t *mn = mnd + DSB_LV_ERROR + 1, *ed = edd + DSB_LV_ERROR + 1;
+	int32_t prev_mn, cur_mn, next_mn, prev_ed, cur_ed, next_ed;
+	int32_t best_score = query_length;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+	for (int i = -DSB_LV_ERROR - 1; i <= DSB_LV_ERROR + 1; i++) {
+		mn[i] = -1;
+		ed[i] = (i > 0) ? i : -i;
+	}
+	mn[DSB_LV_ERROR + 2] = -1;
+	ed[DSB_LV_ERROR + 2] = DSB_LV_ERROR + 2;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+	for (int i = 0; i <= DSB_LV_ERROR; i++) {
+		prev_mn = -1;
+		cur_mn = i - 1;
+		next_mn = mn[-i + 1];
+		prev_ed = i + 1;
+		cur_ed = i;
+		next_ed = ed[-i + 1];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+		for (int j = -i; j <= DSB_LV_ERROR; j++) {
+			if (cur_mn + j < ref_length - 1) {
+				int MAX_mn_ed = cur_mn + 1 - cur_ed;
+				mn[j] = cur_mn + 1;
+				ed[j] = cur_ed + 1;
+				if (MAX_mn_ed < next_mn + 1 - next_ed) {
+					mn[j] = next_mn + 1;
+					ed[j] = next_ed + 1;
+					MAX_mn_ed = next_mn - next_ed;
+				}
+				if (MAX_mn_ed < prev_mn - prev_ed) {
+					mn[j] = prev_mn + 1;
+					ed[j] = prev_ed + 1;
+				}
+			} else {
+				int MAX_mn_ed = cur_mn - cur_ed;
+				mn[j] = cur_mn;
+				ed[j] = cur_ed + 1;
+				if (MAX_mn_ed < prev_mn - prev_ed) {
+					mn[j] = prev_mn;
+					ed[j] = prev_ed + 1;
+					MAX_mn_ed = prev_mn - prev_ed;
+				}
+				if (MAX_mn_ed < next_mn + 1 - next_ed) {
+					mn[j] = next_mn + 1;
+					ed[j] = next_ed + 1;
+				}
+			}
+			int mn_j = DSB_MIN(mn[j], query_length);
+			mn_j = DSB_MIN(mn_j, ref_length - j);
+			for (;;) { /* for (; ref[mn_j + j] == query[mn_j]; mn_j++) */
+				uint64_t x = dsb_win8(R, mn_j + j) ^ dsb_win8(Q, mn_j);
+				if (x) {
+					mn_j += __builtin_ctzll(x) >> 3;
+					break;
+				}
+				mn_j += 8;
+			}
+			mn[j] = mn_j;
+			if (dsb_byte_at(Q, mn_j) == '$' || dsb_byte_at(R, mn_j + j) == '#') {
+				best_score = DSB_MIN(ed[j] - 1, best_score);
+				if (j <= i + 1)
+					return best_score;
+			}
+			prev_mn = cur_mn; cur_mn = next_mn; next_mn = mn[j + 2];
+			prev_ed = cur_ed; cur_ed = next_ed; next_ed = ed[j + 2];
+		}
+	}
+	return best_score;
+}
+
 /* ------------------------------------------------------------------ glibc msort */
 /*
  * glibc 2.35 qsort == top-down merge sort (msort_with_tmp): n1 = n/2, n2 = n - n1, sort
