@@ -28,7 +28,9 @@
 			   ((PH) == DSB_PH_FAST0 || (PH) == DSB_PH_FAST1 || (PH) == DSB_PH_SLOW0 || (PH) == DSB_PH_SLOW1) \
 			   ? DSB_MINW_FAST : DSB_MINW_RESOLVE)
 #define DSB_WIN_LDS_BYTES ((DSB_WIN_BYTES + 15) & ~15)
-#define DSB_DELA_LDS (DSB_WIN_LDS_BYTES + DSB_SMS_LDS * sizeof(dsb_spd_t))
+/* scoring-phase LDS per wave: the reference windows (+ 64 B slack for the 8-byte word reads past
+ * their end), and the sparse-DP prefix when DSB_SMS_IN_LDS */
+#define DSB_DELA_LDS (DSB_WIN_LDS_BYTES + 64 + (DSB_SMS_IN_LDS ? DSB_SMS_LDS * sizeof(dsb_spd_t) : 0))
 static_assert(sizeof(dsb_rstate_t) <= DSB_STATE_BYTES, "per-read phase state must fit its workspace slot");
 
 /* One phase of classify part A (dsb_phase), one lane per read; the read's control state
@@ -79,6 +81,68 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t 
 			atomicAdd(gstats + DSB_ST_STRIDE * PH + k, (unsigned long long)st[k]);
 }
 
+/* The island phase (getIsland, src/cly.c:1231-1263) with two lanes per read: lane 2i scans the
+ * forward strand, lane 2i+1 the reverse strand (search_exist_kmer_M2 + get_seed_vector_M2), and
+ * the pair exchanges its SEARCH_DIRs.  The reference writes the reverse seeds after the forward
+ * ones into one buffer (reverse at L/4, H8): when the forward list runs past L/4 the reverse
+ * lane redoes its pass after the forward stores have completed, so its values win there. */
+template <bool STATS>
+__global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+							   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+							   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+							   dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
+							   unsigned long long *__restrict__ gstats, uint32_t dbg)
+{
+	(void)dbg; (void)ro; (void)n_overflow; (void)gstats;
+	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	uint32_t i = t >> 1, strand = t & 1;
+	if (i >= n) /* both lanes of a pair leave together */
+		return;
+	uint32_t r = order[i];
+	uint32_t L = len[r];
+	uint8_t *base = ws + ws_off[r];
+	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
+	dsb_read_ws w;
+	dsb_ws_init(&w, ix, base, L, cap);
+	dsb_rstate_t *sp = (dsb_rstate_t *)(base + dsb_layout(L, cap).state);
+	dsb_rflags_t f = {0, 0, 0, 0};
+	w.n_anc = 0;
+	w.fast_classify = 1;
+	w.n_hit = 0;
+	w.reached_update = 0;
+	if (L < DSB_MIN_READ_LEN) {
+		f.done = 1;
+	} else {
+		dsb_sdir_t sd;
+		if (strand == 0)
+			dsb_seed_vector(&w, 0, 0, DSB_FORWARD, &sd);
+		else
+			dsb_seed_vector(&w, 1, L >> 2, DSB_REVERSE, &sd);
+		dsb_sdir_t o;
+		o.seed_off = (uint32_t)__shfl_xor((int)sd.seed_off, 1);
+		o.l_seed_v_f = (uint32_t)__shfl_xor((int)sd.l_seed_v_f, 1);
+		o.strand = (uint32_t)__shfl_xor((int)sd.strand, 1);
+		o.direction = (uint32_t)__shfl_xor((int)sd.direction, 1);
+		o.total_score = (uint32_t)__shfl_xor((int)sd.total_score, 1);
+		uint32_t l_fwd = strand == 0 ? sd.l_seed_v_f : o.l_seed_v_f;
+		if (l_fwd > (L >> 2)) { /* forward seeds reach the reverse buffer: the reverse pass goes last */
+			__threadfence();
+			if (strand == 1)
+				dsb_seed_vector(&w, 1, L >> 2, DSB_REVERSE, &sd);
+		}
+		w.sd[0] = strand == 0 ? sd : o;
+		w.sd[1] = strand == 0 ? o : sd;
+		if (w.sd[0].total_score < w.sd[1].total_score) {
+			dsb_sdir_t x = w.sd[0];
+			w.sd[0] = w.sd[1];
+			w.sd[1] = x;
+		}
+		f.both = ((w.sd[0].total_score - w.sd[1].total_score) <= (w.sd[0].total_score >> 3));
+	}
+	if (strand == 0)
+		dsb_state_save(&w, &f, sp);
+}
+
 /* One phase of part A with one wavefront per read (dsb_wave.h), one wave per workgroup:
  * fast seeding (FAST0/FAST1), chaining (RESOLVE_*), scoring (DELA).  The last phase
  * publishes the read's summary like k_phase. */
@@ -113,7 +177,7 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 	if (PH == DSB_PH_DELA && (dbg & 512)) { /* scoring: reference windows and the sparse-DP prefix in LDS */
 		extern __shared__ uint8_t dsb_lds[];
 		w.win = dsb_lds;
-		w.sms_lds = (dsb_spd_t *)(dsb_lds + DSB_WIN_LDS_BYTES);
+		w.sms_lds = DSB_SMS_IN_LDS ? (dsb_spd_t *)(dsb_lds + DSB_WIN_LDS_BYTES + 64) : 0;
 	}
 	int active = dsb_phase_active(&w, &f, ph);
 	if (active) {

@@ -445,7 +445,7 @@ static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
 				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), dbg);
 	else
-		hipLaunchKernelGGL(fn, dim3((m + 63) / 64), dim3(64), 0, s, g->d, cl, g->ws_off.as<uint64_t>(),
+		hipLaunchKernelGGL(fn, dim3(((ph == DSB_PH_ISLAND ? 2 : 1) * m + 63) / 64), dim3(64), 0, s, g->d, cl, g->ws_off.as<uint64_t>(),
 				   g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(), g->cnt.as<uint32_t>(),
 				   g->stats.as<unsigned long long>(), dbg);
 }

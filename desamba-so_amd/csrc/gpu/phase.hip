@@ -22,8 +22,8 @@
 extern "C" dsb_phase_fn DSB_CAT(dsb_phase_kernel_, DSB_PH)(int wave, int stats)
 {
 #if DSB_PH == 0
-	(void)wave;
-	return stats ? k_phase<0, true> : k_phase<0, false>;
+	(void)wave; /* two lanes per read (k_island); launched with 2 x reads threads */
+	return stats ? k_island<true> : k_island<false>;
 #else
 	if (wave)
 		return stats ? k_wave_phase<DSB_PH, true> : k_wave_phase<DSB_PH, false>;
