@@ -999,7 +999,7 @@ DSB_HDN void dsb_slow_classify(dsb_read_ws *w, const dsb_sdir_t *sd)
 }
 
 template <bool SLOW>
-DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, dsb_mem_t *memtmp)
+DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, dsb_mem_t *memtmp, int32_t *lds)
 {
 	const dsb_dindex_t *ix = w->ix;
 	uint32_t lane = dsb_lane();
@@ -1104,6 +1104,13 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 			break;
 		uint64_t mapm = dsb_wballot(st == DSB_SM_MAP);
 		int do_map = mapm != 0 && ((uint32_t)__builtin_popcountll(mapm) >= DSB_SM_MAP_BATCH || mapm == act);
+		if (w->stats && lane == 0) { /* trip counters (stats kernels): trips, map trips, lanes mapping */
+			w->stats[DSB_ST_T_DPM]++;
+			if (do_map) {
+				w->stats[DSB_ST_T_DPS]++;
+				w->stats[DSB_ST_T_FILL] += (uint64_t)__builtin_popcountll(mapm);
+			}
+		}
 		/* ---- MAP: map_seed of hit k_map, batched; its REF_POS entries are spread over the wave.
 		 * Items are numbered owner by owner (lane order), REF_POS order inside an owner; a kept
 		 * Anchor goes to its owner's staging at the owner's count + the number of kept items of
@@ -1120,18 +1127,27 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 				dsb_mem_t *mq = SLOW ? top + k_map : m_r + k_map;
 				if (!SLOW)
 					mq->read_offset = string_index - mq->match_len;
+#ifndef DSB_EXP_NO_PRE
 				dsb_map_seed_pre(w, mq, &s_i, &cx);
+#endif
 			}
 			DSB_T1(DSB_ST_T_BUILD, tp0); /* lane 0: wave clocks in map_seed's prefix / suffix part */
+#ifdef DSB_EXP_NO_ITEMS
+			cx.n_items = 0; /* timing experiment only */
+#endif
 			uint32_t cnt = inmap ? cx.n_items : 0;
 			uint32_t tot, pfx = dsb_wscan(cnt, &tot);
 			uint32_t n_before = w->n_anc;
+			int32_t *own = lds, *omax = lds + DSB_WV; /* LDS: owner lane of each item of a chunk; kept max per owner */
+			omax[lane] = 0;
 			for (uint32_t cb = 0; cb < tot; cb += DSB_WV) {
 				uint32_t it = cb + lane;
-				int o = 0; /* owner: the last lane whose prefix is <= it */
-				for (int step = DSB_WV / 2; step > 0; step >>= 1)
-					if ((uint32_t)dsb_wshfl_any((int)pfx, o + step) <= it)
-						o += step;
+				if (inmap) /* owners label their items of this chunk */
+					for (uint32_t q = DSB_MAX(pfx, cb); q < pfx + cnt && q < cb + DSB_WV; q++)
+						own[q - cb] = (int32_t)lane;
+				dsb_wsync();
+				int o = it < tot ? own[lane] : 0;
+				dsb_wsync();
 				dsb_mapctx_t oc;
 				uint32_t opfx = (uint32_t)dsb_wshfl_any((int)pfx, o);
 				oc.rp_s = ((uint64_t)(uint32_t)dsb_wshfl_any((int)(uint32_t)(cx.rp_s >> 32), o) << 32) |
@@ -1155,7 +1171,9 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 				oc.ref_r = (uint8_t)((pk3 >> 1) & 1);
 				dsb_seedinfo_t os = {bin_read, w->L, (uint16_t)(pk3 >> 16), s_d->direction};
 				dsb_anchor_t an;
+				uint64_t ti0 = DSB_T0();
 				int pass = it < tot ? dsb_map_item(w, &oc, it - opfx, &os, &an) : 0;
+				DSB_T1(DSB_ST_T_MATCH, ti0); /* lane 0: wave clocks in the REF_POS items themselves */
 				uint64_t pm = dsb_wballot(pass);
 				uint32_t start = opfx > cb ? opfx - cb : 0; /* the owner's first item in this chunk */
 				uint64_t before = (lane == 0 ? 0 : (~0ull >> (64 - lane))) & ~(start == 0 ? 0 : (~0ull >> (64 - start)));
@@ -1164,6 +1182,8 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 					w->anc_tmp[(uint64_t)o * S + dest] = an;
 					if (w->stats) w->stats[DSB_ST_ANCHOR]++;
 				}
+				if (pass)
+					dsb_lds_max(omax + o, (int32_t)an.score);
 				/* owners: count their kept items of this chunk */
 				if (inmap) {
 					uint32_t lo = pfx > cb ? pfx - cb : 0, hi = DSB_MIN(pfx + cnt, cb + DSB_WV) - cb;
@@ -1181,9 +1201,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 						w->overflow |= 1;
 						n_before = S;
 					}
-					c_score = 0;
-					for (uint32_t a = w->n_anc; a < n_before; a++)
-						c_score = DSB_MAX(c_score, (int)stg[a].score);
+					c_score = omax[lane];
 					w->n_anc = n_before;
 				}
 				max_score = DSB_MAX(c_score, max_score);
@@ -1469,13 +1487,14 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 }
 
 /* fast_classify / slow_classify with one wavefront per read: the per-lane state machine */
-DSB_HDN void dsb_fast_classify_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset)
+/* lds: 2 x DSB_WV int32 of workgroup-local memory */
+DSB_HDN void dsb_fast_classify_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, int32_t *lds)
 {
-	dsb_seed_sm<false>(w, s_d, hset, w->mem);
+	dsb_seed_sm<false>(w, s_d, hset, w->mem, lds);
 }
-DSB_HDN void dsb_slow_classify_sm(dsb_read_ws *w, const dsb_sdir_t *sd, uint64_t *hset, dsb_mem_t *memtmp)
+DSB_HDN void dsb_slow_classify_sm(dsb_read_ws *w, const dsb_sdir_t *sd, uint64_t *hset, dsb_mem_t *memtmp, int32_t *lds)
 {
-	dsb_seed_sm<true>(w, sd, hset, memtmp);
+	dsb_seed_sm<true>(w, sd, hset, memtmp, lds);
 }
 
 /* ------------------------------------------------------------------ chaining */

@@ -61,6 +61,8 @@ DSB_HD uint64_t dsb_wmax64(uint64_t v)
 	return v;
 }
 DSB_HD uint64_t dsb_wballot(int p) { return __ballot(p); }
+/* *p = max(*p, v) on workgroup-local memory, from any lane */
+DSB_HD void dsb_lds_max(int32_t *p, int32_t v) { atomicMax(p, v); }
 /* value of lane `src` for a per-lane src (ds_bpermute) */
 DSB_HD int dsb_wshfl_any(int v, int src) { return __shfl(v, src); }
 /* value of lane `src`; src must be wave-uniform (v_readlane) */
@@ -75,6 +77,7 @@ DSB_HD uint64_t dsb_wmax64(uint64_t v) { return v; }
 DSB_HD uint64_t dsb_wballot(int p) { return p ? 1 : 0; }
 DSB_HD int dsb_wshfl(int v, int src) { (void)src; return v; }
 DSB_HD int dsb_wshfl_any(int v, int src) { (void)src; return v; }
+DSB_HD void dsb_lds_max(int32_t *p, int32_t v) { if (v > *p) *p = v; }
 #endif
 
 #endif

@@ -613,6 +613,10 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			HIP_OK(hipMemcpyAsync(g->sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, s));
 			HIP_OK(hipMemcpyAsync(g->wo2.p, wo2.data(), 8 * wo2.size(), hipMemcpyHostToDevice, s));
 			uint32_t m = (uint32_t)sel.size();
+			if (m == 0) {
+				snprintf(err, errn, "overflow reported by the phase kernels but no read carries the flag");
+				return -1;
+			}
 			k_encode<<<m, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, g->sel.as<uint32_t>(), m);
 			if (tw2)
 				k_seed<<<(uint32_t)((tw2 * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
