@@ -379,7 +379,10 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_spset_t *s) { return dsb_spset_inse
  * 500-entry array" (a wrap is `l == m -> l = 0`, i.e. the array forgets everything), so a
  * generation counter replaces clearing.  Slot = gen << 40 | node (BWT rows < 2^40), 0 = empty.
  */
-#define DSB_HSET_SLOTS 1024
+#ifndef DSB_HSET_LOG2
+#define DSB_HSET_LOG2 9
+#endif
+#define DSB_HSET_SLOTS (1u << DSB_HSET_LOG2) /* > 500: the reference's set never holds more */
 typedef struct { uint64_t *tab; uint32_t stride, gen; int l, m; } dsb_hset_t;
 DSB_HD void dsb_set_reset(dsb_hset_t *s)
 {
@@ -392,7 +395,7 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_hset_t *s)
 		s->l = 0;
 		s->gen++;
 	}
-	uint32_t h = (uint32_t)((node * 0x9E3779B97F4A7C15ull) >> 54);
+	uint32_t h = (uint32_t)((node * 0x9E3779B97F4A7C15ull) >> (64 - DSB_HSET_LOG2));
 	uint64_t key = ((uint64_t)s->gen << 40) | node;
 	for (;;) {
 		uint64_t v = s->tab[(uint64_t)h * s->stride];

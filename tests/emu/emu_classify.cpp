@@ -106,10 +106,12 @@ int main(int argc, char **argv)
 				for (int ph = 0; ph < DSB_PH_DELA; ph++) {
 					if ((ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) && dsb_phase_active(&w, &f, ph)) {
 						memset(hset, 0, 8ull * DSB_HSET_SLOTS * 64);
-						dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset);
+						static int32_t sm_lds[2];
+						dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, sm_lds);
 					} else if ((ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) && dsb_phase_active(&w, &f, ph)) {
 						memset(hset, 0, 8ull * DSB_HSET_SLOTS * 64);
-						dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem);
+						static int32_t sm_lds2[2];
+						dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem, sm_lds2);
 					} else
 						dsb_phase<true>(&w, &f, ph);
 				}
