@@ -377,13 +377,22 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_spset_t *s) { return dsb_spset_inse
  * The same set as an open-addressing hash (one per lane of the wave-cooperative seeding):
  * membership == "inserted since the last reset or since the last wrap of the reference's
  * 500-entry array" (a wrap is `l == m -> l = 0`, i.e. the array forgets everything), so a
- * generation counter replaces clearing.  Slot = gen << 40 | node (BWT rows < 2^40), 0 = empty.
+ * generation counter replaces clearing.  A slot is {node, gen64}: gen64 = the launch tag (host
+ * run epoch << 32 | phase << 28) | the lane's generation.  Epochs only grow within a process,
+ * so slots written by earlier runs never compare equal and read as empty: the table is never
+ * cleared (kernels.hip clears the workspace if the 32-bit epoch ever wraps).
  */
 #ifndef DSB_HSET_LOG2
 #define DSB_HSET_LOG2 9
 #endif
 #define DSB_HSET_SLOTS (1u << DSB_HSET_LOG2) /* > 500: the reference's set never holds more */
-typedef struct { uint64_t *tab; uint32_t stride, gen; int l, m; } dsb_hset_t;
+#define DSB_HSET_SLOT_U64 2
+typedef struct { uint64_t *tab; uint32_t stride, gen; int l, m; uint64_t tag; } dsb_hset_t;
+/* launch tag: the host's run epoch (dsb_dindex_t.run_epoch, 32 bits) and the phase */
+DSB_HD uint64_t dsb_hset_tag(const dsb_dindex_t *ix, int ph)
+{
+	return ((uint64_t)ix->run_epoch << 32) | ((uint64_t)(ph & 15) << 28);
+}
 DSB_HD void dsb_set_reset(dsb_hset_t *s)
 {
 	s->l = 0;
@@ -396,13 +405,15 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_hset_t *s)
 		s->gen++;
 	}
 	uint32_t h = (uint32_t)((node * 0x9E3779B97F4A7C15ull) >> (64 - DSB_HSET_LOG2));
-	uint64_t key = ((uint64_t)s->gen << 40) | node;
+	uint64_t g = s->tag | (s->gen & 0x0fffffffu);
 	for (;;) {
-		uint64_t v = s->tab[(uint64_t)h * s->stride];
-		if (v == key)
+		uint64_t *slot = s->tab + (uint64_t)h * s->stride;
+		uint64_t sn = slot[0], sg = slot[1];
+		if (sg == g && sn == node)
 			return 0;
-		if ((uint32_t)(v >> 40) != s->gen) {
-			s->tab[(uint64_t)h * s->stride] = key;
+		if (sg != g) {
+			slot[0] = node;
+			slot[1] = g;
 			s->l++;
 			return 1;
 		}
@@ -1009,7 +1020,8 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	uint32_t n_sv = s_d->l_seed_v_f;
 	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV; /* dbg 32: tiny staging (tests the replay) */
 	dsb_anchor_t *stg = w->anc_tmp + (uint64_t)lane * S;
-	dsb_hset_t hs = {hset + lane, DSB_WV, 0, 0, 500};
+	dsb_hset_t hs = {hset + DSB_HSET_SLOT_U64 * lane, DSB_HSET_SLOT_U64 * DSB_WV, 0, 0, 500,
+			 dsb_hset_tag(ix, SLOW ? 4 : 1)};
 	uint8_t l_ek = (uint8_t)ix->l_ek;
 	int min_index = DSB_MIN_MEM_LEN_FAST - l_ek;
 	/* bwt_MEM_search parameters: fast src/cly.c:1500-1501, slow src/cly.c:1568-1570 */

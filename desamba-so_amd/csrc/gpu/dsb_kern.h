@@ -183,16 +183,12 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 	if (active) {
 		if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
 			uint64_t *hset = (uint64_t *)(base + lay.hset);
-			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
-				hset[k] = 0;
-			__syncthreads();
+			/* no clearing: slots carry the launch tag (dsb_set_insert) */
 			__shared__ int32_t sm_lds[2 * 64];
 			dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, sm_lds);
 		} else if (ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) {
 			uint64_t *hset = (uint64_t *)(base + lay.hset);
-			for (uint32_t k = lane; k < DSB_HSET_SLOTS * 64; k += 64)
-				hset[k] = 0;
-			__syncthreads();
+			/* no clearing: slots carry the launch tag (dsb_set_insert) */
 			__shared__ int32_t sm_lds2[2 * 64];
 			dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem, sm_lds2);
 		} else

@@ -65,7 +65,7 @@ DSB_HD dsb_ws_layout dsb_layout(uint32_t L, dsb_caps_t cap)
 	o.win = p; p = dsb_al(p + DSB_WIN_BYTES);
 	o.mem = p; p = dsb_al(p + sizeof(dsb_mem_t) * 16 * 64); /* 16 MEM results per lane (slow seeding) */
 	o.spset = p; p = dsb_al(p + 8 * 512);
-	o.hset = p; p = dsb_al(p + 8ull * DSB_HSET_SLOTS * 64); /* per-lane sp_set hashes (wave seeding) */
+	o.hset = p; p = dsb_al(p + 8ull * DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS * 64); /* per-lane sp_set hashes */
 	o.state = p; p = dsb_al(p + DSB_STATE_BYTES); /* dsb_rstate_t: state between phase launches */
 	o.total = p;
 	return o;

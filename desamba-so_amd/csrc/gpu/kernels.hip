@@ -227,6 +227,7 @@ struct dsb_gpu_dev {
 	dsb_dindex_t *d;         /* device copy */
 	std::vector<void *> allocs;
 	dbuf ws_off, scale, ws, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2;
+	uint32_t epoch = 0;      /* run counter tagging the seeding sp_set slots (dsb_dindex_t.run_epoch) */
 };
 
 template <typename T>
@@ -520,6 +521,18 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	dsb_read_out_t *ro = b->ro.data();
 	std::vector<dsb_hit_out_t> &hv = b->hits;
 	size_t budget = ws_budget(g);
+	/* a new run epoch: seeding sp_set slots written by earlier runs never match this run's tags;
+	 * if the 32-bit epoch ever wraps, the workspace is cleared once so no old tag can repeat */
+	g->epoch++;
+	if (g->epoch == 0) {
+		g->epoch = 1;
+		if (g->ws.p)
+			HIP_OK(hipMemsetAsync(g->ws.p, 0, g->ws.cap, s));
+	}
+	{
+		uint32_t ep = g->epoch;
+		HIP_OK(hipMemcpy(&g->d->run_epoch, &ep, 4, hipMemcpyHostToDevice));
+	}
 	int carry = *max_read_l;
 	int l_ek = ix->l_ek;
 	for (uint64_t cb = 0; cb < n;) {

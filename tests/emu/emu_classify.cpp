@@ -105,11 +105,11 @@ int main(int argc, char **argv)
 				uint64_t *hset = (uint64_t *)(arena.data() + lay.hset);
 				for (int ph = 0; ph < DSB_PH_DELA; ph++) {
 					if ((ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) && dsb_phase_active(&w, &f, ph)) {
-						memset(hset, 0, 8ull * DSB_HSET_SLOTS * 64);
+						memset(hset, 0, 8ull * DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS * 64);
 						static int32_t sm_lds[2];
 						dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, sm_lds);
 					} else if ((ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) && dsb_phase_active(&w, &f, ph)) {
-						memset(hset, 0, 8ull * DSB_HSET_SLOTS * 64);
+						memset(hset, 0, 8ull * DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS * 64);
 						static int32_t sm_lds2[2];
 						dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem, sm_lds2);
 					} else
