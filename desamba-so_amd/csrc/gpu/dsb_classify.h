@@ -1830,10 +1830,39 @@ DSB_HD void dsb_get_ref_win(dsb_read_ws *w, uint8_t *ref_str, uint64_t uni_offse
 			length = 0;
 		uint64_t b0 = uni_offset >> 2;
 		uint32_t odd = (uint32_t)(uni_offset & 3);
-		for (uint32_t k = lane; k < length; k += DSB_WV) {
-			uint32_t pos = odd + k;
-			uint8_t b = dsb_ref_byte(w->ix, b0 + (pos >> 2));
-			ref_str[k] = (b >> (6 - 2 * (pos & 3))) & 0x3;
+#ifndef DSB_WIN_WORDS
+#define DSB_WIN_WORDS 0 /* 8-base stores raise the scoring kernel's spills 40 -> 105: off */
+#endif
+		if (DSB_WIN_WORDS && ((uintptr_t)ref_str & 7) == 0) {
+			/* 8 bases per lane: one 8-byte window of the packed reference, one 8-byte store
+			 * (bytes past `length` are left as they are: they hold earlier window contents) */
+			for (uint32_t k0 = lane * 8; k0 < length; k0 += 8 * DSB_WV) {
+				uint64_t pos0 = uni_offset + k0;
+				uint64_t B = pos0 >> 2;
+				uint64_t out = 0;
+				if (B + 16 <= w->ix->ref_bin_padded) {
+					uint64_t v = __builtin_bswap64(dsb_ld8u(w->ix->ref_bin + B));
+					uint32_t sh = (uint32_t)(pos0 & 3);
+					for (int j = 0; j < 8; j++)
+						out |= ((v >> (62 - 2 * (sh + j))) & 3) << (8 * j);
+				} else {
+					for (int j = 0; j < 8; j++) {
+						uint64_t p = pos0 + j;
+						out |= (uint64_t)((dsb_ref_byte(w->ix, p >> 2) >> (6 - 2 * (p & 3))) & 3) << (8 * j);
+					}
+				}
+				if (k0 + 8 <= length)
+					*(uint64_t *)(ref_str + k0) = out;
+				else
+					for (uint32_t j = 0; j < length - k0; j++)
+						ref_str[k0 + j] = (uint8_t)(out >> (8 * j));
+			}
+		} else {
+			for (uint32_t k = lane; k < length; k += DSB_WV) {
+				uint32_t pos = odd + k;
+				uint8_t b = dsb_ref_byte(w->ix, b0 + (pos >> 2));
+				ref_str[k] = (b >> (6 - 2 * (pos & 3))) & 0x3;
+			}
 		}
 		dsb_wsync();
 	}
@@ -2149,8 +2178,22 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 						for (int k = 0; k < DSB_S_A_KMER_L; k++) k0 = (k0 << 2) | c0[k];
 						kmer = (k0 << 2) >> (2 * (i - 3));
 					}
-					for (int j = DSB_MAX(4, i - 12); j <= i; j++)
-						kmer |= ((uint64_t)t_str[(int)t_len - DSB_S_A_KMER_L - j] << 16) >> (2 * (i - j));
+#ifndef DSB_REVK_WORDS
+#define DSB_REVK_WORDS 1
+#endif
+					if (!DSB_REVK_WORDS) {
+						for (int j = DSB_MAX(4, i - 12); j <= i; j++)
+							kmer |= ((uint64_t)t_str[(int)t_len - DSB_S_A_KMER_L - j] << 16) >> (2 * (i - j));
+					} else { /* bytes t_str[t_len - 9 - j], j = i .. i-12, are c_t_str[d], d = i - j: two word loads */
+						uint64_t w0 = dsb_ld8u(c_t_str), w1 = dsb_ld8u(c_t_str + 8);
+						int dmax = DSB_MIN(12, i - 4);
+						for (int d = 0; d <= 12; d++) {
+							if (d > dmax)
+								break;
+							uint64_t b = (d < 8 ? (w0 >> (8 * d)) : (w1 >> (8 * (d - 8)))) & 0xff;
+							kmer |= (b << 16) >> (2 * d);
+						}
+					}
 				}
 				if (w->stats) w->stats[DSB_ST_LOOKUP]++;
 				for (uint32_t nd = heads[kmer & KEY_MASK], hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
