@@ -102,6 +102,8 @@ typedef struct {
 	dsb_chain_t *hit_tmp;
 	dsb_spd_t *sms; uint32_t n_sms;
 	dsb_spd_t *sms_lds;     /* wave scoring: the first DSB_SMS_LDS sms entries live in LDS */
+	uint64_t *lds_key;      /* wave chaining: anchor sort keys / ids in LDS (DSB_SORT_LDS entries), or 0 */
+	uint32_t *lds_id;
 	uint32_t *hh[2], *hn[2]; /* read 9-mer hash per strand: list heads per key, one node per position */
 	dsb_sch_t *sch;         /* 256 + 2*400 */
 	uint8_t *win;           /* DSB_WIN_BYTES: sdp_middle ref[2000] and sdp_right/left ref[1000] windows */
@@ -1590,6 +1592,7 @@ DSB_HD void dsb_chain_insert_M2(dsb_read_ws *w, uint32_t ai)
 /* Anchor_cmp_by_chr_ID_and_pos under glibc msort == stable ascending sort by
  * (ref_ID, direction, ref_offset).  WAVE: bitonic sort of (key, index) pairs (a total order,
  * so the same permutation as any stable sort), keys/indices staged in hit_tmp. */
+#define DSB_SORT_LDS 512
 template <bool WAVE>
 DSB_HD void dsb_sort_anchors(dsb_read_ws *w)
 {
@@ -1608,6 +1611,10 @@ DSB_HD void dsb_sort_anchors(dsb_read_ws *w)
 	while (N < n) N <<= 1;
 	uint64_t *key = (uint64_t *)w->hit_tmp;
 	uint32_t *id = (uint32_t *)(key + N);
+	if (w->lds_key && N <= DSB_SORT_LDS) { /* small sorts run in LDS */
+		key = w->lds_key;
+		id = w->lds_id;
+	}
 	for (uint32_t k = lane; k < N; k += DSB_WV) {
 		if (k < n) {
 			key[k] = ((uint64_t)A[k].ref_ID << 33) | ((uint64_t)(A[k].direction != 0) << 32) | A[k].ref_offset;

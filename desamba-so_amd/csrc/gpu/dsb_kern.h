@@ -191,6 +191,12 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 			/* no clearing: slots carry the launch tag (dsb_set_insert) */
 			__shared__ int32_t sm_lds2[2 * 64];
 			dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem, sm_lds2);
+		} else if (ph == DSB_PH_RESOLVE_F || ph == DSB_PH_RESOLVE_S0 || ph == DSB_PH_RESOLVE_S1) {
+			__shared__ uint64_t sort_key[DSB_SORT_LDS];
+			__shared__ uint32_t sort_id[DSB_SORT_LDS];
+			w.lds_key = sort_key;
+			w.lds_id = sort_id;
+			dsb_phase<true>(&w, &f, ph);
 		} else
 			dsb_phase<true>(&w, &f, ph);
 	}
