@@ -1802,6 +1802,66 @@ DSB_HD void dsb_sort_chains(dsb_read_ws *w, Cmp cmp)
 	for (uint32_t k = 0; k < n; k++) H[k] = w->hit_tmp[k];
 }
 
+/*
+ * chain_cmp_by_score as a stable sort on a key (the comparator is a total preorder, so glibc's
+ * stable merge sort and any stable sort give the same permutation): with_top_anchor first, then
+ * score = sum_score + 2 (q_ed - q_st) - 4 indel (int arithmetic of src/cly.c:37-51) descending.
+ * WAVE + LDS: bitonic sort of (key, index) pairs over the wave for <= DSB_SORT_LDS chains.
+ */
+template <bool WAVE>
+DSB_HD void dsb_sort_chains_by_score(dsb_read_ws *w)
+{
+	uint32_t n = w->n_hit;
+	if (n <= 1)
+		return;
+	uint32_t N = 1;
+	while (N < n) N <<= 1;
+	if (!WAVE || !w->lds_key || N > DSB_SORT_LDS) {
+		dsb_sort_chains(w, [](const dsb_chain_t *a, const dsb_chain_t *b) -> int { return dsb_chain_cmp_by_score(a, b); });
+		return;
+	}
+	uint32_t lane = dsb_lane();
+	uint64_t *key = w->lds_key;
+	uint32_t *id = w->lds_id;
+	dsb_chain_t *H = w->hit;
+	for (uint32_t k = lane; k < N; k += DSB_WV) {
+		if (k < n) {
+			int sc = (int)(H[k].sum_score + ((H[k].q_ed - H[k].q_st) << 1));
+			sc -= (int)(H[k].indel << 2);
+			uint64_t k2 = (uint64_t)((int64_t)0x7fffffff - (int64_t)sc);
+			key[k] = ((uint64_t)(H[k].with_top_anchor ? 0 : 1) << 33) | k2;
+			id[k] = k;
+		} else {
+			key[k] = ~0ull;
+			id[k] = 0xffffffffu;
+		}
+	}
+	dsb_wsync();
+	for (uint32_t size = 2; size <= N; size <<= 1) {
+		for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+			for (uint32_t t = lane; t < N / 2; t += DSB_WV) {
+				uint32_t lo = ((t / stride) * stride << 1) + (t % stride);
+				uint32_t hi = lo + stride;
+				int asc = ((lo & size) == 0);
+				uint64_t ka = key[lo], kb = key[hi];
+				uint32_t ia = id[lo], ib = id[hi];
+				int gt = (ka > kb) || (ka == kb && ia > ib);
+				if (gt == asc) {
+					key[lo] = kb; key[hi] = ka;
+					id[lo] = ib; id[hi] = ia;
+				}
+			}
+			dsb_wsync();
+		}
+	}
+	for (uint32_t k = lane; k < n; k += DSB_WV)
+		w->hit_tmp[k] = H[id[k]];
+	dsb_wsync();
+	for (uint32_t k = lane; k < n; k += DSB_WV)
+		H[k] = w->hit_tmp[k];
+	dsb_wsync();
+}
+
 /* resolve_tree, src/cly.c:325-348 */
 template <bool WAVE>
 DSB_HDN void dsb_resolve_tree(dsb_read_ws *w)
@@ -1815,7 +1875,7 @@ DSB_HDN void dsb_resolve_tree(dsb_read_ws *w)
 	if (w->overflow)
 		return;
 	if (w->n_hit > 1)
-		dsb_sort_chains(w, [](const dsb_chain_t *a, const dsb_chain_t *b) -> int { return dsb_chain_cmp_by_score(a, b); });
+		dsb_sort_chains_by_score<WAVE>(w);
 	uint32_t rst_num = DSB_MIN(5u, w->n_hit);
 	while (rst_num < w->n_hit && w->hit[rst_num].with_top_anchor == 1)
 		rst_num++;
