@@ -2421,7 +2421,44 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 			p->t_pos = c_a->ref_offset;
 			p->len = c_a->mtch_len - DSB_S_A_KMER_L + 1;
 			uint64_t tdp0 = DSB_T0();
-			if (w->n_sms > 1) {
+			if (WAVE && !DSB_SEQ(w, 4) && w->n_sms > 1 && w->n_sms <= DSB_WV) {
+				/* register-resident DP: lane l holds node l (q, t, len, score); node cs's fields
+				 * come by v_readlane, its predecessors are lanes < cs, its score goes back to
+				 * lane cs — no memory traffic inside the node loop */
+				uint32_t lane = dsb_lane(), n = w->n_sms;
+				uint32_t nq = 0, nt = 0, nl = 0, nsc = 0;
+				if (lane < n) {
+					const dsb_spd_t *me = dsb_sms(w, lane);
+					nq = me->q_pos; nt = me->t_pos; nl = me->len; nsc = me->score;
+				}
+				int pre_q_ed = (int)(nq + nl + DSB_S_A_KMER_L - 1);
+				int pre_t_ed = (int)(nt + nl + DSB_S_A_KMER_L - 1);
+				for (uint32_t cs = 1; cs < n; cs++) {
+					uint32_t cq = (uint32_t)dsb_wshfl((int)nq, (int)cs), ct = (uint32_t)dsb_wshfl((int)nt, (int)cs);
+					uint32_t cl = (uint32_t)dsb_wshfl((int)nl, (int)cs);
+					int max_score = (int)cl;
+					uint32_t max_q = cq + DSB_MAX_SMS_OVERLAP;
+					uint32_t max_t = ct + DSB_MAX_SMS_OVERLAP;
+					int cand = INT32_MIN;
+					if (lane < cs && !((uint32_t)pre_q_ed > max_q) && !((uint32_t)pre_t_ed > max_t)) {
+						int indel = (int)(nq - nt - (max_q - max_t));
+						int ABS_indel = DSB_ABS(indel);
+						if (ABS_indel <= 200) {
+							cand = (int)(nsc + cl - (uint32_t)(ABS_indel >> 3));
+							if ((uint32_t)pre_q_ed > cq || (uint32_t)pre_t_ed > ct)
+								cand -= DSB_MAX(pre_q_ed - (int)cq, pre_t_ed - (int)ct);
+						}
+					}
+					int best = dsb_wmax(cand);
+					max_score = DSB_MAX(max_score, best);
+					score = DSB_MAX(max_score, score);
+					if (lane == cs)
+						nsc = (uint32_t)max_score;
+				}
+				if (lane < n && lane > 0)
+					dsb_sms(w, lane)->score = nsc;
+				dsb_wsync();
+			} else if (w->n_sms > 1) {
 				for (uint32_t cs = 1; cs < w->n_sms; cs++) {
 					dsb_spd_t *c_spd = dsb_sms(w, cs);
 					int max_score = (int)c_spd->len;
