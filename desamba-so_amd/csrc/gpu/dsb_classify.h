@@ -94,6 +94,7 @@ typedef struct {
 	uint32_t L;             /* read length */
 	uint8_t *bin;           /* F at bin[0..L), R at bin[L..2L); guard before/after */
 	const uint64_t *exF, *exR; /* exist bits per k-mer position (K_seed output) */
+	const uint32_t *pre;    /* k-mer & 0x3FFFFFF per position (K_seed output): F at [0, L), R at [L, 2L) */
 	dsb_seed_t *seeds;      /* (L>>1)+20 (+spill) entries; R seeds at L>>2 (src/cly.c:1238,1252) */
 	dsb_anchor_t *anc; uint32_t n_anc;
 	dsb_anchor_t *anc_tmp;
@@ -1396,8 +1397,8 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 					st = DSB_SM_FIN;
 			} else {
 				int kmer_index = (int)seed_off + j;
-				uint64_t kmer = dsb_kmer_at(bin_read + kmer_index, l_ek, ix->single_base_max);
-				uint64_t pre_v = kmer & DSB_PRE_IDX_MASK;
+				/* (kmer_at(...) & DSB_PRE_IDX_MASK), computed once per position by k_seed */
+				uint64_t pre_v = w->pre[(s_d->strand ? w->L : 0) + (uint32_t)kmer_index];
 				string_index = kmer_index + l_ek - 1;
 				if (w->stats) w->stats[DSB_ST_MEMSEARCH]++;
 				sp = ix->hash_index[pre_v];

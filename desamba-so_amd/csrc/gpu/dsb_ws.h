@@ -39,7 +39,7 @@ DSB_HD uint32_t dsb_ex_words(uint32_t L) { return (L >> 6) + 2; }
 DSB_HD uint32_t dsb_seed_cap(uint32_t L) { return (L >> 1) + 20 + L / 3 + 64; }
 
 typedef struct {
-	uint64_t bin, exF, exR, seeds, anc, anc_tmp, sidx, stmp, hit, hit_tmp, sms, hash, sch, win, mem, spset, hset, state, total;
+	uint64_t bin, exF, exR, pre, seeds, anc, anc_tmp, sidx, stmp, hit, hit_tmp, sms, hash, sch, win, mem, spset, hset, state, total;
 	uint32_t kl;
 } dsb_ws_layout;
 
@@ -51,6 +51,7 @@ DSB_HD dsb_ws_layout dsb_layout(uint32_t L, dsb_caps_t cap)
 	o.bin = p; p = dsb_al(p + DSB_BIN_GUARD + 2ull * L + DSB_BIN_TAIL);
 	o.exF = p; p = dsb_al(p + 8ull * dsb_ex_words(L));
 	o.exR = p; p = dsb_al(p + 8ull * dsb_ex_words(L));
+	o.pre = p; p = dsb_al(p + 8ull * L); /* u32 13-mer prefix value per k-mer position, F then R */
 	o.seeds = p; p = dsb_al(p + sizeof(dsb_seed_t) * (uint64_t)dsb_seed_cap(L));
 	o.anc = p; p = dsb_al(p + sizeof(dsb_anchor_t) * (uint64_t)cap.anc);
 	o.anc_tmp = p; p = dsb_al(p + DSB_MAX(sizeof(dsb_anchor_t) * (uint64_t)cap.anc, sizeof(dsb_mem_t) * 256ull));
@@ -80,6 +81,7 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 	w->bin = base + o.bin + DSB_BIN_GUARD;
 	w->exF = (const uint64_t *)(base + o.exF);
 	w->exR = (const uint64_t *)(base + o.exR);
+	w->pre = (const uint32_t *)(base + o.pre);
 	w->seeds = (dsb_seed_t *)(base + o.seeds);
 	w->anc = (dsb_anchor_t *)(base + o.anc);
 	w->n_anc = 0;

@@ -87,6 +87,7 @@ int main(int argc, char **argv)
 					memset(ex[s], 0, 8 * dsb_ex_words(L));
 					for (uint32_t k = 0; k < lk; k++) {
 						uint64_t km = dsb_kmer_at(w.bin + s * L + k, d.l_ek, d.single_base_max);
+						((uint32_t *)w.pre)[s * L + k] = (uint32_t)(km & DSB_PRE_IDX_MASK);
 						if (dsb_exist_kmer(&d, km)) ex[s][k >> 6] |= 1ull << (k & 63);
 					}
 				}
