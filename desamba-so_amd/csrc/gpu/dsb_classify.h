@@ -2225,46 +2225,71 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 		uint32_t lane = dsb_lane();
 		if (!dsb_win_ok(w, t_str, isForward ? 0 : -51, (int64_t)t_len + 64, 2))
 			return;
+#ifndef DSB_MATCH_PF
+#define DSB_MATCH_PF 0
+#endif
+		/* the probe 9-mer of position i = 4m and the window byte it starts at */
+		auto probe = [&](int m, const uint8_t *&cts) -> uint64_t {
+			int i = 4 * m;
+			uint64_t kmer = 0;
+			if (isForward) { /* ((k << 2) | c) & 0x3ffff rolled: only the 9 bytes at i remain */
+				cts = t_str + i;
+				kmer = dsb_q9mer(cts);
+			} else {
+				/* (k >> 2) | (c << 16) rolled without a mask: bytes > 3 (pattern/stale window
+				 * bytes, sdp_left's t_offset_global == 0 case) linger for up to 12 steps */
+				cts = t_str + ((int)t_len - DSB_S_A_KMER_L - i);
+				if (i < 16) {
+					const uint8_t *c0 = t_str + ((int)t_len - DSB_S_A_KMER_L - 4);
+					uint64_t k0 = 0;
+					for (int k = 0; k < DSB_S_A_KMER_L; k++) k0 = (k0 << 2) | c0[k];
+					kmer = (k0 << 2) >> (2 * (i - 3));
+				}
+				/* bytes t_str[t_len - 9 - j], j = i .. i-12, are cts[d], d = i - j: two word loads */
+				uint64_t w0 = dsb_ld8u(cts), w1 = dsb_ld8u(cts + 8);
+				int dmax = DSB_MIN(12, i - 4);
+				for (int d = 0; d <= 12; d++) {
+					if (d > dmax)
+						break;
+					uint64_t b = (d < 8 ? (w0 >> (8 * d)) : (w1 >> (8 * (d - 8)))) & 0xff;
+					kmer |= (b << 16) >> (2 * d);
+				}
+			}
+			return kmer;
+		};
+		/* software pipeline: the next batch's probe and list head are loaded before this
+		 * batch's lists are walked, so that their latency overlaps the walk */
+		const uint8_t *n_cts = t_str;
+		uint64_t n_kmer = 0;
+		uint32_t n_head = DSB_HEMPTY;
+		if (DSB_MATCH_PF && (int)lane + 1 <= n_i) {
+			n_kmer = probe((int)lane + 1, n_cts);
+			n_head = heads[n_kmer & KEY_MASK];
+		}
 		for (int mb = 0; mb < n_i; mb += DSB_WV) {
 			int m = mb + (int)lane + 1;
 			uint32_t cnt = 0;
 			dsb_spd_t e0 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
 			const uint8_t *c_t_str = t_str;
 			uint64_t kmer = 0;
+			uint32_t head = DSB_HEMPTY;
 			int i = 4 * m;
-			if (m <= n_i) {
-				if (isForward) { /* ((k << 2) | c) & 0x3ffff rolled: only the 9 bytes at i remain */
-					c_t_str = t_str + i;
-					kmer = dsb_q9mer(c_t_str);
-				} else {
-					/* (k >> 2) | (c << 16) rolled without a mask: bytes > 3 (pattern/stale window
-					 * bytes, sdp_left's t_offset_global == 0 case) linger for up to 12 steps */
-					c_t_str = t_str + ((int)t_len - DSB_S_A_KMER_L - i);
-					if (i < 16) {
-						const uint8_t *c0 = t_str + ((int)t_len - DSB_S_A_KMER_L - 4);
-						uint64_t k0 = 0;
-						for (int k = 0; k < DSB_S_A_KMER_L; k++) k0 = (k0 << 2) | c0[k];
-						kmer = (k0 << 2) >> (2 * (i - 3));
-					}
-#ifndef DSB_REVK_WORDS
-#define DSB_REVK_WORDS 1
-#endif
-					if (!DSB_REVK_WORDS) {
-						for (int j = DSB_MAX(4, i - 12); j <= i; j++)
-							kmer |= ((uint64_t)t_str[(int)t_len - DSB_S_A_KMER_L - j] << 16) >> (2 * (i - j));
-					} else { /* bytes t_str[t_len - 9 - j], j = i .. i-12, are c_t_str[d], d = i - j: two word loads */
-						uint64_t w0 = dsb_ld8u(c_t_str), w1 = dsb_ld8u(c_t_str + 8);
-						int dmax = DSB_MIN(12, i - 4);
-						for (int d = 0; d <= 12; d++) {
-							if (d > dmax)
-								break;
-							uint64_t b = (d < 8 ? (w0 >> (8 * d)) : (w1 >> (8 * (d - 8)))) & 0xff;
-							kmer |= (b << 16) >> (2 * d);
-						}
-					}
+			if (DSB_MATCH_PF) {
+				c_t_str = n_cts;
+				kmer = n_kmer;
+				head = n_head;
+				n_head = DSB_HEMPTY;
+				if (m + DSB_WV <= n_i) {
+					n_kmer = probe(m + DSB_WV, n_cts);
+					n_head = heads[n_kmer & KEY_MASK];
 				}
+			} else if (m <= n_i) {
+				kmer = probe(m, c_t_str);
+				head = heads[kmer & KEY_MASK];
+			}
+			if (m <= n_i) {
 				if (w->stats) w->stats[DSB_ST_LOOKUP]++;
-				for (uint32_t nd = heads[kmer & KEY_MASK], hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
+				for (uint32_t nd = head, hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
 					if (w->stats) w->stats[DSB_ST_NODE]++;
 					hv = hnode[nd];
 					if (!dsb_hmatch(hv, kmer, key_len))
