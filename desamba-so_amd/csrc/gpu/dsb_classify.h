@@ -1982,29 +1982,34 @@ DSB_HD void dsb_sc_hash_idx(dsb_read_ws *w)
 }
 
 /*
- * Read 9-mer hash node (one u32 per read position, heads[key] = first position, EMPTY = none):
- *   key_len < 18:  bits 0-23 next position with the same key (0xFFFFFF = none), bits 24-31 the
- *                  k-mer bits above the key (kmer >> key_len, at most 8 bits)
- *   key_len == 18: the next position (EMPTY = none); the key is the whole 18-bit k-mer
- * (positions are < 2^17 whenever key_len < 18).  Equality with a probe k-mer whose key bits
- * select the list is then (probe >> key_len) == stored high bits, which is also false for the
- * unmasked probes (> 0x3ffff) of the backward scan, as in the reference's 64-bit compare.
+ * Read 9-mer hash (per strand): heads[key] = the entry of the first position with that key,
+ * node[p] = the entry of the position after p in p's list (EMPTY = none).  An entry is
+ *   key_len < 18:  bits 0-22 the position, bit 23 "a successor follows" (node[position] is
+ *                  valid), bits 24-31 the k-mer bits above the key (kmer >> key_len, <= 8 bits)
+ *   key_len == 18: the position (the key is the whole 18-bit k-mer; node[] is always read)
+ * (positions are < 2^17 whenever key_len < 18).  A probe whose list has a single element thus
+ * costs one load; equality with the probe k-mer is (probe >> key_len) == stored high bits, which
+ * is also false for the unmasked probes (> 0x3ffff) of the backward scan, as in the
+ * reference's 64-bit compare.
  */
 #define DSB_HEMPTY 0xffffffffu
-DSB_HD uint32_t dsb_hnode(uint32_t next, uint32_t kmer, int kl)
+DSB_HD uint32_t dsb_hentry(uint32_t pos, uint32_t kmer, int has_next, int kl)
 {
-	return kl >= 18 ? next : ((next & 0xffffffu) | ((kmer >> kl) << 24));
+	return kl >= 18 ? pos : (pos | ((uint32_t)has_next << 23) | ((kmer >> kl) << 24));
 }
-DSB_HD uint32_t dsb_hnext(uint32_t node, int kl)
+DSB_HD uint32_t dsb_hpos(uint32_t e, int kl)
+{
+	return kl >= 18 ? e : (e & 0x7fffffu);
+}
+DSB_HD uint32_t dsb_hstep(uint32_t e, const uint32_t *node, int kl)
 {
 	if (kl >= 18)
-		return node;
-	uint32_t n = node & 0xffffffu;
-	return n == 0xffffffu ? DSB_HEMPTY : n;
+		return node[e];
+	return (e & 0x800000u) ? node[e & 0x7fffffu] : DSB_HEMPTY;
 }
-DSB_HD int dsb_hmatch(uint32_t node, uint64_t kmer, int kl)
+DSB_HD int dsb_hmatch(uint32_t e, uint64_t kmer, int kl)
 {
-	return (kmer >> kl) == (uint64_t)(kl >= 18 ? 0u : (node >> 24));
+	return (kmer >> kl) == (uint64_t)(kl >= 18 ? 0u : (e >> 24));
 }
 
 /* the read 9-mer at c: kmer(c) = (OR_k q[c+k] << 2(8-k)) & 0x3ffff, the rolled value */
@@ -2048,8 +2053,9 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 			for (int c_pos = n_pos - 1; c_pos >= 0; c_pos--) {
 				uint32_t kmer = dsb_q9mer(q + c_pos);
 				uint32_t key = kmer & KEY_MASK;
-				node[c_pos] = dsb_hnode(heads[key], kmer, key_len);
-				heads[key] = (uint32_t)c_pos;
+				uint32_t old = heads[key];
+				node[c_pos] = old;
+				heads[key] = dsb_hentry((uint32_t)c_pos, kmer, old != DSB_HEMPTY, key_len);
 			}
 		} else {
 			/* chunks of 64 positions from the end; inside a chunk each lane finds the nearest
@@ -2071,12 +2077,14 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 						else if (o > (int)lane) nxt = o;
 					}
 				}
+				uint32_t old = act ? heads[key] : DSB_HEMPTY;
+				uint32_t ent = dsb_hentry((uint32_t)c_pos, kmer, nxt >= 0 || old != DSB_HEMPTY, key_len);
+				uint32_t nent = (uint32_t)dsb_wshfl_any((int)ent, nxt >= 0 ? nxt : (int)lane);
 				if (act) {
 					if (w->stats) w->stats[DSB_ST_HASH_B] += 12;
-					uint32_t succ = (nxt >= 0) ? (uint32_t)(cb + nxt) : heads[key];
-					node[c_pos] = dsb_hnode(succ, kmer, key_len);
+					node[c_pos] = nxt >= 0 ? nent : old;
 					if (!has_prev)
-						heads[key] = (uint32_t)c_pos;
+						heads[key] = ent;
 				}
 				dsb_wsync();
 			}
@@ -2157,11 +2165,10 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			kmer = ((kmer << 2) | c_t_str[DSB_S_A_KMER_L - 1]) & 0x3ffff;
 			if ((i & 0x03) != 0)
 				continue;
-			for (uint32_t nd = heads[kmer & KEY_MASK], hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
-				hv = hnode[nd];
-				if (!dsb_hmatch(hv, kmer, key_len))
+			for (uint32_t e = heads[kmer & KEY_MASK]; e != DSB_HEMPTY; e = dsb_hstep(e, hnode, key_len)) {
+				if (!dsb_hmatch(e, kmer, key_len))
 					continue;
-				uint32_t q_pos = nd;
+				uint32_t q_pos = dsb_hpos(e, key_len);
 				if (q_pos >= q_bg && q_pos <= q_ed) {
 					int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, 4);
 					if (back_len < 4 || i == 4) {
@@ -2190,11 +2197,10 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			kmer = (kmer >> 2) | ((uint64_t)c_t_str[0] << 16); /* bit2_preKmerMOVE, no mask */
 			if ((i & 0x03) != 0)
 				continue;
-			for (uint32_t nd = heads[kmer & KEY_MASK], hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
-				hv = hnode[nd];
-				if (!dsb_hmatch(hv, kmer, key_len))
+			for (uint32_t e = heads[kmer & KEY_MASK]; e != DSB_HEMPTY; e = dsb_hstep(e, hnode, key_len)) {
+				if (!dsb_hmatch(e, kmer, key_len))
 					continue;
-				uint32_t q_pos = nd;
+				uint32_t q_pos = dsb_hpos(e, key_len);
 				if (q_pos >= q_bg && q_pos <= q_ed) {
 					int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L, 1, 4);
 					if (forward_len < 4 || i == 4) {
@@ -2289,12 +2295,11 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			}
 			if (m <= n_i) {
 				if (w->stats) w->stats[DSB_ST_LOOKUP]++;
-				for (uint32_t nd = head, hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
+				for (uint32_t he = head; he != DSB_HEMPTY; he = dsb_hstep(he, hnode, key_len)) {
 					if (w->stats) w->stats[DSB_ST_NODE]++;
-					hv = hnode[nd];
-					if (!dsb_hmatch(hv, kmer, key_len))
+					if (!dsb_hmatch(he, kmer, key_len))
 						continue;
-					uint32_t q_pos = nd;
+					uint32_t q_pos = dsb_hpos(he, key_len);
 					if (!(q_pos >= q_bg && q_pos <= q_ed))
 						continue;
 					dsb_spd_t e;
@@ -2349,11 +2354,10 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			if (cnt > 1) { dsb_spd_t *d = dsb_sms(w, dst + 1); d->len = e1.len; d->q_pos = e1.q_pos; d->t_pos = e1.t_pos; }
 			if (cnt > 2) { /* rare: more than two matches for one position, walk the list again */
 				uint32_t k = 0;
-				for (uint32_t nd = heads[kmer & KEY_MASK], hv; nd != DSB_HEMPTY; nd = dsb_hnext(hv, key_len)) {
-					hv = hnode[nd];
-					if (!dsb_hmatch(hv, kmer, key_len))
+				for (uint32_t e = heads[kmer & KEY_MASK]; e != DSB_HEMPTY; e = dsb_hstep(e, hnode, key_len)) {
+					if (!dsb_hmatch(e, kmer, key_len))
 						continue;
-					uint32_t q_pos = nd;
+					uint32_t q_pos = dsb_hpos(e, key_len);
 					if (!(q_pos >= q_bg && q_pos <= q_ed))
 						continue;
 					int ok = 0;
