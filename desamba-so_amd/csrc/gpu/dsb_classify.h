@@ -105,6 +105,7 @@ typedef struct {
 	dsb_spd_t *sms_lds;     /* wave scoring: the first DSB_SMS_LDS sms entries live in LDS */
 	uint64_t *lds_key;      /* wave chaining: anchor sort keys / ids in LDS (DSB_SORT_LDS entries), or 0 */
 	uint32_t *lds_id;
+	uint8_t *lds_hb;        /* wave read-hash build: DSB_HB_LDS lane-id bytes in LDS (key groups of a chunk), or 0 */
 	uint32_t *hh[2], *hn[2]; /* read 9-mer hash per strand: list heads per key, one node per position */
 	dsb_sch_t *sch;         /* 256 + 2*400 */
 	uint8_t *win;           /* DSB_WIN_BYTES: sdp_middle ref[2000] and sdp_right/left ref[1000] windows */
@@ -1993,6 +1994,7 @@ DSB_HD void dsb_sc_hash_idx(dsb_read_ws *w)
  * reference's 64-bit compare.
  */
 #define DSB_HEMPTY 0xffffffffu
+#define DSB_HB_LDS 4096 /* LDS bytes of the wave hash build's key-group slots (power of two) */
 DSB_HD uint32_t dsb_hentry(uint32_t pos, uint32_t kmer, int has_next, int kl)
 {
 	return kl >= 18 ? pos : (pos | ((uint32_t)has_next << 23) | ((kmer >> kl) << 24));
@@ -2070,11 +2072,38 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 				uint32_t kmer = act ? dsb_q9mer(q + c_pos) : 0;
 				int key = act ? (int)(kmer & KEY_MASK) : -1 - (int)lane;
 				int has_prev = 0, nxt = -1;
-				for (int o = DSB_WV - 1; o >= 0; o--) {
-					int k2 = dsb_wshfl(key, o);
-					if (k2 == key) {
-						if (o < (int)lane) has_prev = 1;
-						else if (o > (int)lane) nxt = o;
+				if (w->lds_hb) {
+					/* every lane writes its id to a byte slot of its key's low bits and reads it
+					 * back: lanes sharing a key all lost, or lost to the one of them that won, so
+					 * walking the (few) losers and their winners finds every group */
+					uint8_t *hb = w->lds_hb + (key & (DSB_HB_LDS - 1));
+					if (act) *hb = (uint8_t)lane;
+					dsb_wsync();
+					int won = act ? (int)*hb : (int)lane;
+					uint64_t lost = dsb_wballot(won != (int)lane);
+					nxt = DSB_WV;
+					while (lost) {
+						int o = __builtin_ctzll(lost);
+						lost &= lost - 1;
+						int w2 = dsb_wshfl(won, o);
+						int k2 = dsb_wshfl(key, o), k3 = dsb_wshfl(key, w2);
+						if (k2 == key) {
+							if (o < (int)lane) has_prev = 1;
+							else if (o > (int)lane) nxt = DSB_MIN(nxt, o);
+						}
+						if (k3 == key) {
+							if (w2 < (int)lane) has_prev = 1;
+							else if (w2 > (int)lane) nxt = DSB_MIN(nxt, w2);
+						}
+					}
+					if (nxt == DSB_WV) nxt = -1;
+				} else {
+					for (int o = DSB_WV - 1; o >= 0; o--) {
+						int k2 = dsb_wshfl(key, o);
+						if (k2 == key) {
+							if (o < (int)lane) has_prev = 1;
+							else if (o > (int)lane) nxt = o;
+						}
 					}
 				}
 				uint32_t old = act ? heads[key] : DSB_HEMPTY;

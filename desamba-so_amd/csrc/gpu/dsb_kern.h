@@ -185,6 +185,8 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 			uint64_t *hset = (uint64_t *)(base + lay.hset);
 			/* no clearing: slots carry the launch tag (dsb_set_insert) */
 			__shared__ int32_t sm_lds[2 * 64];
+			__shared__ uint8_t hb_lds_f[DSB_HB_LDS];
+			w.lds_hb = hb_lds_f;
 			dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, sm_lds);
 		} else if (ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) {
 			uint64_t *hset = (uint64_t *)(base + lay.hset);
@@ -196,6 +198,10 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 			__shared__ uint32_t sort_id[DSB_SORT_LDS];
 			w.lds_key = sort_key;
 			w.lds_id = sort_id;
+			dsb_phase<true>(&w, &f, ph);
+		} else if (ph == DSB_PH_DELA) {
+			__shared__ uint8_t hb_lds[DSB_HB_LDS];
+			w.lds_hb = hb_lds;
 			dsb_phase<true>(&w, &f, ph);
 		} else
 			dsb_phase<true>(&w, &f, ph);
