@@ -125,6 +125,7 @@ int dsb_classify_text(void *idx, const char *text, uint64_t text_n, int format, 
 		timing->n_retry = gt.n_retry;
 		timing->n_chunks = gt.n_chunks;
 		timing->seed_positions = gt.seed_positions;
+		timing->n_launch_dela = gt.n_launch_dela;
 		for (int k = 0; k < DSB_N_STATS; k++) timing->stats[k] = gt.stats[k];
 	}
 	free(ro);
@@ -199,6 +200,7 @@ static void copy_timing(dsb_timing_t *t, const dsb_gpu_timing *gt)
 	t->n_retry = gt->n_retry;
 	t->n_chunks = gt->n_chunks;
 	t->seed_positions = gt->seed_positions;
+	t->n_launch_dela = gt->n_launch_dela;
 	for (int k = 0; k < DSB_N_STATS; k++) t->stats[k] = gt->stats[k];
 }
 

@@ -25,6 +25,7 @@ typedef struct {
 	double ms_phase[12];  /* k_phase<ph> times (ms_classA = their sum) */
 	uint64_t n_reads, n_bases, n_retry, n_chunks;
 	uint64_t seed_positions; /* k-mer positions probed by the seed kernel (both strands) */
+	uint64_t n_launch_dela;  /* launches of the scoring kernel (2 per chunk when part A was split) */
 	uint64_t stats[DSB_N_STATS]; /* work counters DSB_ST_*: [32*ph, 32*ph+32) phase ph, [288,320) k_classB */
 } dsb_gpu_timing;
 

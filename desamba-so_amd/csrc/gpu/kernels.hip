@@ -223,12 +223,13 @@ struct dbuf {
 struct dsb_gpu_dev {
 	int device;
 	hipStream_t stream;
-	hipEvent_t ev_a, ev_b;
+	hipStream_t stream2;     /* scoring of the reads that skip slow seeding, beside the slow phases */
+	hipEvent_t ev_a, ev_b, ev_fork, ev_r0, ev_r1;
 	pthread_mutex_t mu;
 	dsb_dindex_t h;          /* host copy holding device pointers */
 	dsb_dindex_t *d;         /* device copy */
 	std::vector<void *> allocs;
-	dbuf ws_off, scale, ws, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2;
+	dbuf ws_off, scale, ws, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2;
 	uint32_t epoch = 0;      /* run counter tagging the seeding sp_set slots (dsb_dindex_t.run_epoch) */
 };
 
@@ -278,6 +279,14 @@ extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
 	HIP_OK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
 	HIP_OK(hipEventCreate(&g->ev_a));
 	HIP_OK(hipEventCreate(&g->ev_b));
+	{ /* the split-off scoring yields to the slow phases */
+		int least = 0, greatest = 0;
+		HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+		HIP_OK(hipStreamCreateWithPriority(&g->stream2, hipStreamNonBlocking, least));
+	}
+	HIP_OK(hipEventCreate(&g->ev_fork));
+	HIP_OK(hipEventCreate(&g->ev_r0));
+	HIP_OK(hipEventCreate(&g->ev_r1));
 	dsb_dindex_t &h = g->h;
 	memset(&h, 0, sizeof(h));
 	/* occ lines (128 B per 256 BWT symbols, re-laid out by the loader) + one zero line */
@@ -327,11 +336,15 @@ extern "C" void dsb_gpu_free(dsb_index *ix)
 	for (void *p : g->allocs)
 		hipFree(p);
 	dbuf *bs[] = {&g->ws_off, &g->scale, &g->ws, &g->order, &g->word_off, &g->ro, &g->mrl, &g->hits,
-		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2};
+		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2};
 	for (dbuf *b : bs)
 		b->release();
 	hipEventDestroy(g->ev_a);
 	hipEventDestroy(g->ev_b);
+	hipEventDestroy(g->ev_fork);
+	hipEventDestroy(g->ev_r0);
+	hipEventDestroy(g->ev_r1);
+	hipStreamDestroy(g->stream2);
 	hipStreamDestroy(g->stream);
 	pthread_mutex_destroy(&g->mu);
 	delete g;
@@ -433,9 +446,10 @@ static uint32_t wave_phases(void)
 
 /* one phase of part A over the reads order[0..m) */
 static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl, uint8_t *wsb, const uint32_t *order,
-			 uint32_t m)
+			 uint32_t m, hipStream_t s = 0)
 {
-	hipStream_t s = g->stream;
+	if (!s)
+		s = g->stream;
 	int wave = (int)((wave_phases() >> ph) & 1);
 	dsb_phase_fn fn = phase_kernel_at(ph, wave, stats);
 	if (!fn) { /* a lane-per-read phase variant that is not compiled in (build with DSB_LANE_PHASES=1) */
@@ -494,6 +508,100 @@ static int batch_upload(dsb_gpu_dev *g, const dsb_reads_t *reads, dsb_gpu_batch 
 	T.n_reads = n;
 	T.n_bases = tot;
 	return 0;
+}
+
+/* after resolve_f: reads[order[t]] -> slow list (slow seeding still to run) or rest list (scoring
+ * next); one atomic per wave, lane order kept inside a wave (per-read results do not depend on
+ * the processing order) */
+__global__ __launch_bounds__(64) void k_split(const uint32_t *__restrict__ len, const uint64_t *__restrict__ ws_off,
+					      const uint32_t *__restrict__ scale, const uint8_t *__restrict__ ws,
+					      const uint32_t *__restrict__ order, uint32_t n, uint32_t *__restrict__ slow_list,
+					      uint32_t *__restrict__ rest_list, uint32_t *__restrict__ cnt2)
+{
+	uint32_t t = blockIdx.x * 64 + threadIdx.x, lane = threadIdx.x;
+	int act = t < n, slow = 0;
+	uint32_t r = 0;
+	if (act) {
+		r = order[t];
+		uint32_t L = len[r];
+		dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, scale[r]));
+		const dsb_rstate_t *sp = (const dsb_rstate_t *)(ws + ws_off[r] + lay.state);
+		slow = !sp->f.done && !sp->overflow && sp->f.run_slow;
+	}
+	uint64_t ms = __ballot(act && slow), mr = __ballot(act && !slow);
+	uint32_t bs = 0, br = 0;
+	if (lane == 0) {
+		bs = atomicAdd(cnt2, (uint32_t)__builtin_popcountll(ms));
+		br = atomicAdd(cnt2 + 1, (uint32_t)__builtin_popcountll(mr));
+	}
+	bs = (uint32_t)__shfl((int)bs, 0);
+	br = (uint32_t)__shfl((int)br, 0);
+	uint64_t lt = lane == 0 ? 0 : (~0ull >> (64 - lane));
+	if (act && slow)
+		slow_list[bs + (uint32_t)__builtin_popcountll(ms & lt)] = r;
+	else if (act)
+		rest_list[br + (uint32_t)__builtin_popcountll(mr & lt)] = r;
+}
+
+static int split_slow(void)
+{
+	static int v = -1;
+	if (v < 0)
+		v = getenv("DSB_NO_SPLIT") ? 0 : 1;
+	return v;
+}
+
+/* The slow phases touch ~2% of the reads and leave most of the GPU idle: after resolve_f the
+ * reads are split, the scoring of the rest runs on a second stream while the slow phases and
+ * then the slow reads' scoring run on the first.  Returns 1 when the rest of part A ran here,
+ * 0 when there was nothing to split (the caller continues phase by phase), -1 on error. */
+static int run_split(dsb_gpu_dev *g, bool stats, const uint32_t *cl, uint8_t *wsb, uint32_t cn, dsb_gpu_timing &T,
+		     char *err, size_t errn)
+{
+	hipStream_t s = g->stream;
+	if (g->slist.ensure(4ull * cn + 4, err, errn) || g->rlist.ensure(4ull * cn + 4, err, errn) ||
+	    g->cnt2.ensure(64, err, errn))
+		return -1;
+	HIP_OK(hipMemsetAsync(g->cnt2.p, 0, 8, s));
+	k_split<<<(cn + 63) / 64, 64, 0, s>>>(cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
+					       g->order.as<uint32_t>(), cn, g->slist.as<uint32_t>(), g->rlist.as<uint32_t>(),
+					       g->cnt2.as<uint32_t>());
+	HIP_OK(hipGetLastError());
+	uint32_t c2[2] = {0, 0};
+	HIP_OK(hipMemcpyAsync(c2, g->cnt2.p, 8, hipMemcpyDeviceToHost, s));
+	HIP_OK(hipStreamSynchronize(s));
+	if (c2[0] + c2[1] != cn) {
+		snprintf(err, errn, "split: %u + %u reads for a chunk of %u", c2[0], c2[1], cn);
+		return -1;
+	}
+	if (c2[0] == 0 || c2[1] == 0)
+		return 0;
+	/* slow0's few workgroups are queued before the scoring grid so that they are dispatched first */
+	hipEventRecord(g->ev_fork, s);
+	hipEventRecord(g->ev_a, s);
+	launch_phase(g, DSB_PH_SLOW0, stats, cl, wsb, g->slist.as<uint32_t>(), c2[0]);
+	HIP_OK(hipStreamWaitEvent(g->stream2, g->ev_fork, 0));
+	hipEventRecord(g->ev_r0, g->stream2);
+	launch_phase(g, DSB_PH_DELA, stats, cl, wsb, g->rlist.as<uint32_t>(), c2[1], g->stream2);
+	hipEventRecord(g->ev_r1, g->stream2);
+	HIP_OK(hipGetLastError());
+	T.ms_phase[DSB_PH_SLOW0] += ev_ms(g);
+	for (int ph = DSB_PH_SLOW0 + 1; ph < DSB_PH_N; ph++) {
+		hipEventRecord(g->ev_a, s);
+		launch_phase(g, ph, stats, cl, wsb, g->slist.as<uint32_t>(), c2[0]);
+		T.ms_phase[ph] += ev_ms(g);
+		HIP_OK(hipGetLastError());
+	}
+	HIP_OK(hipStreamWaitEvent(s, g->ev_r1, 0));
+	hipEventRecord(g->ev_b, s);
+	HIP_OK(hipEventSynchronize(g->ev_b));
+	float wall = 0, rest = 0;
+	hipEventElapsedTime(&wall, g->ev_fork, g->ev_b);
+	hipEventElapsedTime(&rest, g->ev_r0, g->ev_r1);
+	T.ms_phase[DSB_PH_DELA] += rest; /* both scoring launches; ms_classA takes the overlapped wall time */
+	T.ms_classA += wall;
+	T.n_launch_dela += 2;
+	return 1;
 }
 
 static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on,
@@ -577,13 +685,24 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			HIP_OK(hipGetLastError());
 		}
 		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
-		for (int ph = 0; ph < DSB_PH_N; ph++) {
+		/* island, fast seeding, resolve: every read */
+		int ph_next = DSB_PH_N;
+		for (int ph = 0; ph < ph_next; ph++) {
 			hipEventRecord(g->ev_a, s);
 			launch_phase(g, ph, stats_on != 0, cl, wsb, g->order.as<uint32_t>(), cn);
 			float ms = ev_ms(g);
 			T.ms_phase[ph] += ms;
 			T.ms_classA += ms;
+			if (ph == DSB_PH_DELA)
+				T.n_launch_dela++;
 			HIP_OK(hipGetLastError());
+			if (ph == DSB_PH_RESOLVE_F && split_slow()) {
+				int r = run_split(g, stats_on != 0, cl, wsb, cn, T, err, errn);
+				if (r < 0)
+					return -1;
+				if (r == 1) /* the rest of part A ran split */
+					break;
+			}
 		}
 		HIP_OK(hipGetLastError());
 		uint32_t n_over = 0;

@@ -26,7 +26,8 @@ class Timing(C.Structure):
                 ("ms_classA", C.c_double), ("ms_classB", C.c_double), ("ms_phase", C.c_double * 12),
                 ("n_reads", C.c_uint64),
                 ("n_bases", C.c_uint64), ("n_retry", C.c_uint64), ("n_chunks", C.c_uint64),
-                ("seed_positions", C.c_uint64), ("stats", C.c_uint64 * 320)]
+                ("seed_positions", C.c_uint64), ("n_launch_dela", C.c_uint64),
+                ("stats", C.c_uint64 * 320)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("stats", "pad", "ms_phase")}

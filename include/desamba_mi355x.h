@@ -19,6 +19,7 @@ typedef struct {
 	double ms_phase[12];   /* classify part A per phase (island, fast0/1, resolve, slow0/1, ...) */
 	uint64_t n_reads, n_bases, n_retry, n_chunks;
 	uint64_t seed_positions; /* k-mer positions probed by k_seed (both strands) */
+	uint64_t n_launch_dela;  /* launches of the scoring kernel k_wave_phase<8> (2 per chunk when split) */
 	uint64_t stats[320];   /* work counters: [32*ph, +32) phase ph of part A, [288,320) k_classB */
 } dsb_timing_t;
 
