@@ -229,7 +229,7 @@ struct dsb_gpu_dev {
 	dsb_dindex_t h;          /* host copy holding device pointers */
 	dsb_dindex_t *d;         /* device copy */
 	std::vector<void *> allocs;
-	dbuf ws_off, scale, ws, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2;
+	dbuf ws_off, scale, ws, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2, woA, woB;
 	uint32_t epoch = 0;      /* run counter tagging the seeding sp_set slots (dsb_dindex_t.run_epoch) */
 };
 
@@ -336,7 +336,7 @@ extern "C" void dsb_gpu_free(dsb_index *ix)
 	for (void *p : g->allocs)
 		hipFree(p);
 	dbuf *bs[] = {&g->ws_off, &g->scale, &g->ws, &g->order, &g->word_off, &g->ro, &g->mrl, &g->hits,
-		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2};
+		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2, &g->woA, &g->woB};
 	for (dbuf *b : bs)
 		b->release();
 	hipEventDestroy(g->ev_a);
@@ -543,6 +543,14 @@ __global__ __launch_bounds__(64) void k_split(const uint32_t *__restrict__ len, 
 		rest_list[br + (uint32_t)__builtin_popcountll(mr & lt)] = r;
 }
 
+static int split_seed(void)
+{
+	static int v = -1;
+	if (v < 0)
+		v = getenv("DSB_NO_SPLIT_SEED") ? 0 : 1;
+	return v;
+}
+
 static int split_slow(void)
 {
 	static int v = -1;
@@ -670,13 +678,57 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		for (uint32_t i = 0; i < cn; i++) order[i] = i;
 		std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return len[cb + a] > len[cb + b]; });
 		HIP_OK(hipMemcpyAsync(g->order.p, order.data(), 4ull * cn, hipMemcpyHostToDevice, s));
-		uint64_t tw = seed_words(len, cb, nullptr, cn, l_ek, word_off, &T.seed_positions);
-		HIP_OK(hipMemcpyAsync(g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
 		uint8_t *wsb = g->ws.as<uint8_t>();
 		hipEventRecord(g->ev_a, s);
 		k_encode<<<cn, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, nullptr, cn);
 		T.ms_encode += ev_ms(g);
 		HIP_OK(hipGetLastError());
+		int ph0 = 0; /* first phase still to run */
+		uint64_t tw = 0;
+		if (split_seed() && cn >= 2048) {
+			/* the island scan of the longer half runs on the second stream while k_seed probes the
+			 * shorter half (the island scan keeps few waves in flight, k_seed is bandwidth work) */
+			uint32_t h = cn / 2;
+			std::vector<uint64_t> woA, woB;
+			uint64_t twA = seed_words(len, cb, order.data(), h, l_ek, woA, &T.seed_positions);
+			uint64_t twB = seed_words(len, cb, order.data() + h, cn - h, l_ek, woB, &T.seed_positions);
+			if (g->woA.ensure(8 * woA.size() + 16, err, errn) || g->woB.ensure(8 * woB.size() + 16, err, errn))
+				return -1;
+			HIP_OK(hipMemcpyAsync(g->woA.p, woA.data(), 8 * woA.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(hipMemcpyAsync(g->woB.p, woB.data(), 8 * woB.size(), hipMemcpyHostToDevice, s));
+			const uint32_t *oA = g->order.as<uint32_t>(), *oB = oA + h;
+			hipEventRecord(g->ev_a, s);
+			if (twA)
+				k_seed<<<(uint32_t)((twA * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
+											      g->woA.as<uint64_t>(), oA, h, twA);
+			hipEventRecord(g->ev_fork, s);
+			HIP_OK(hipStreamWaitEvent(g->stream2, g->ev_fork, 0));
+			hipEventRecord(g->ev_r0, g->stream2);
+			launch_phase(g, DSB_PH_ISLAND, stats_on != 0, cl, wsb, oA, h, g->stream2);
+			hipEventRecord(g->ev_r1, g->stream2);
+			if (twB)
+				k_seed<<<(uint32_t)((twB * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
+											      g->woB.as<uint64_t>(), oB, cn - h, twB);
+			HIP_OK(hipGetLastError());
+			hipEventRecord(g->ev_b, s);
+			HIP_OK(hipEventSynchronize(g->ev_b));
+			float ms_s = 0;
+			hipEventElapsedTime(&ms_s, g->ev_a, g->ev_b);
+			T.ms_seed += ms_s;
+			hipEventRecord(g->ev_a, s);
+			launch_phase(g, DSB_PH_ISLAND, stats_on != 0, cl, wsb, oB, cn - h);
+			HIP_OK(hipStreamWaitEvent(s, g->ev_r1, 0));
+			float ms_i = ev_ms(g), ms_ia = 0;
+			hipEventElapsedTime(&ms_ia, g->ev_r0, g->ev_r1);
+			T.ms_phase[DSB_PH_ISLAND] += ms_i; /* the wall time after k_seed; island A overlapped it */
+			T.ms_classA += ms_i;
+			(void)ms_ia;
+			HIP_OK(hipGetLastError());
+			ph0 = DSB_PH_ISLAND + 1;
+		} else {
+			tw = seed_words(len, cb, nullptr, cn, l_ek, word_off, &T.seed_positions);
+			HIP_OK(hipMemcpyAsync(g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
+		}
 		if (tw) {
 			hipEventRecord(g->ev_a, s);
 			k_seed<<<(uint32_t)((tw * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
@@ -686,8 +738,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		}
 		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
 		/* island, fast seeding, resolve: every read */
-		int ph_next = DSB_PH_N;
-		for (int ph = 0; ph < ph_next; ph++) {
+		for (int ph = ph0; ph < DSB_PH_N; ph++) {
 			hipEventRecord(g->ev_a, s);
 			launch_phase(g, ph, stats_on != 0, cl, wsb, g->order.as<uint32_t>(), cn);
 			float ms = ev_ms(g);
