@@ -234,10 +234,17 @@ int dsb_batch_run(void *idx, dsb_batch *b, int *max_read_l, dsb_timing_t *timing
 
 int dsb_batch_format(void *idx, dsb_batch *b, int format, char **output, uint64_t *output_n)
 {
+	return dsb_batch_format_range(idx, b, format, 0, b->reads.n, output, output_n);
+}
+
+int dsb_batch_format_range(void *idx, dsb_batch *b, int format, uint64_t lo, uint64_t hi, char **output,
+			   uint64_t *output_n)
+{
 	const dsb_read_out_t *ro = dsb_gpu_batch_ro(b->g);
 	const dsb_hit_out_t *hits = dsb_gpu_batch_hits(b->g);
 	dsb_str out = {0, 0, 0};
-	for (uint64_t i = 0; i < b->reads.n; i++)
+	if (hi > b->reads.n) hi = b->reads.n;
+	for (uint64_t i = lo; i < hi; i++)
 		dsb_format_read(&out, idx, &b->reads, i, ro + i, hits + ro[i].hit_off, format, 5);
 	*output_n = out.l;
 	*output = calloc(out.l + 1, 1);
@@ -289,6 +296,14 @@ int dsb_batch_taxa(void *idx, dsb_batch *b, int flag, uint32_t *tid_out, uint64_
 	}
 	free(rec_tid);
 	free(rec_score);
+	return 0;
+}
+
+int dsb_batch_carry(dsb_batch *b, int32_t *carry_out)
+{
+	const int32_t *c = dsb_gpu_batch_carry(b->g);
+	for (uint64_t i = 0; i < b->reads.n; i++)
+		carry_out[i] = c ? c[i] : 0;
 	return 0;
 }
 

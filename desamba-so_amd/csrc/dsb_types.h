@@ -67,7 +67,6 @@ typedef struct {
 	const int *Q_MEM;            /* DSB_Q_MEM_PAD ints */
 	const int *Q_LV;             /* [20][20] row-major: Q_LV[ed*20 + len] */
 	int filter_min_length, filter_min_score, filter_min_score_LV3;
-	uint32_t run_epoch;          /* set by the host before each run (seeding sp_set slot tags) */
 } dsb_dindex_t;
 
 /* Output record per hit (what output_one_result_sam needs, cly_mt.c:229-327) */

@@ -120,6 +120,7 @@ typedef struct {
 	/* optional counters for algorithmic-byte accounting (bench) */
 	uint64_t *stats;
 	uint32_t dbg;           /* diagnostics: force sequential variants of the wave loops */
+	uint32_t launch_tag;    /* unique per kernel launch (host counter, never 0): seeding sp_set slot tags */
 } dsb_read_ws;
 
 enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, DSB_ST_REFPOS,
@@ -381,10 +382,12 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_spset_t *s) { return dsb_spset_inse
  * The same set as an open-addressing hash (one per lane of the wave-cooperative seeding):
  * membership == "inserted since the last reset or since the last wrap of the reference's
  * 500-entry array" (a wrap is `l == m -> l = 0`, i.e. the array forgets everything), so a
- * generation counter replaces clearing.  A slot is {node, gen64}: gen64 = the launch tag (host
- * run epoch << 32 | phase << 28) | the lane's generation.  Epochs only grow within a process,
- * so slots written by earlier runs never compare equal and read as empty: the table is never
- * cleared (kernels.hip clears the workspace if the 32-bit epoch ever wraps).
+ * generation counter replaces clearing.  A slot is {node, gen64}: gen64 = the launch tag << 32 |
+ * the lane's generation.  Launch tags only grow within a process, so slots written by earlier
+ * launches never compare equal and read as empty: the table is never cleared (kernels.hip
+ * clears the workspace if the 32-bit tag counter ever wraps).  Within one launch a lane's
+ * generation holds at most 500 entries (the reference's wrap), so a probe always finds a slot
+ * of another generation among the 512.
  */
 #ifndef DSB_HSET_LOG2
 #define DSB_HSET_LOG2 9
@@ -392,10 +395,12 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_spset_t *s) { return dsb_spset_inse
 #define DSB_HSET_SLOTS (1u << DSB_HSET_LOG2) /* > 500: the reference's set never holds more */
 #define DSB_HSET_SLOT_U64 2
 typedef struct { uint64_t *tab; uint32_t stride, gen; int l, m; uint64_t tag; } dsb_hset_t;
-/* launch tag: the host's run epoch (dsb_dindex_t.run_epoch, 32 bits) and the phase */
-DSB_HD uint64_t dsb_hset_tag(const dsb_dindex_t *ix, int ph)
+/* slot tag: the launch's tag (a host counter bumped for every phase launch, so two launches —
+ * FAST0/FAST1, SLOW0/SLOW1, later chunks reusing the same workspace bytes, overflow re-runs —
+ * never share one) in the high word, the lane's generation in the low word */
+DSB_HD uint64_t dsb_hset_tag(const dsb_read_ws *w)
 {
-	return ((uint64_t)ix->run_epoch << 32) | ((uint64_t)(ph & 15) << 28);
+	return (uint64_t)w->launch_tag << 32;
 }
 DSB_HD void dsb_set_reset(dsb_hset_t *s)
 {
@@ -409,7 +414,7 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_hset_t *s)
 		s->gen++;
 	}
 	uint32_t h = (uint32_t)((node * 0x9E3779B97F4A7C15ull) >> (64 - DSB_HSET_LOG2));
-	uint64_t g = s->tag | (s->gen & 0x0fffffffu);
+	uint64_t g = s->tag | s->gen;
 	for (;;) {
 		uint64_t *slot = s->tab + (uint64_t)h * s->stride;
 		uint64_t sn = slot[0], sg = slot[1];
@@ -1025,7 +1030,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV; /* dbg 32: tiny staging (tests the replay) */
 	dsb_anchor_t *stg = w->anc_tmp + (uint64_t)lane * S;
 	dsb_hset_t hs = {hset + DSB_HSET_SLOT_U64 * lane, DSB_HSET_SLOT_U64 * DSB_WV, 0, 0, 500,
-			 dsb_hset_tag(ix, SLOW ? 4 : 1)};
+			 dsb_hset_tag(w)};
 	uint8_t l_ek = (uint8_t)ix->l_ek;
 	int min_index = DSB_MIN_MEM_LEN_FAST - l_ek;
 	/* bwt_MEM_search parameters: fast src/cly.c:1500-1501, slow src/cly.c:1568-1570 */

@@ -49,6 +49,7 @@ int dsb_gpu_batch_run(dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stat
 		      char *err, size_t errn);
 const dsb_read_out_t *dsb_gpu_batch_ro(const dsb_gpu_batch *b);
 const dsb_hit_out_t *dsb_gpu_batch_hits(const dsb_gpu_batch *b);
+const int32_t *dsb_gpu_batch_carry(const dsb_gpu_batch *b);
 uint64_t dsb_gpu_batch_n(const dsb_gpu_batch *b);
 uint64_t dsb_gpu_batch_bases(const dsb_gpu_batch *b);
 void dsb_gpu_batch_free(dsb_index *ix, dsb_gpu_batch *b);

@@ -40,12 +40,14 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t 
 					       const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 					       uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 					       dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
-					       unsigned long long *__restrict__ gstats, uint32_t dbg)
+					       unsigned long long *__restrict__ gstats, uint32_t dbg,
+									      uint32_t tag)
 {
 	(void)dbg;
 	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= n)
 		return;
+	(void)tag;
 	uint32_t r = order[t];
 	uint32_t L = len[r];
 	uint8_t *base = ws + ws_off[r];
@@ -91,9 +93,10 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 							   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 							   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 							   dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
-							   unsigned long long *__restrict__ gstats, uint32_t dbg)
+							   unsigned long long *__restrict__ gstats, uint32_t dbg,
+									      uint32_t tag)
 {
-	(void)dbg; (void)ro; (void)n_overflow; (void)gstats;
+	(void)dbg; (void)ro; (void)n_overflow; (void)gstats; (void)tag;
 	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
 	uint32_t i = t >> 1, strand = t & 1;
 	if (i >= n) /* both lanes of a pair leave together */
@@ -151,7 +154,8 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 						    const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 						    uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 						    dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
-						    unsigned long long *__restrict__ gstats, uint32_t dbg)
+						    unsigned long long *__restrict__ gstats, uint32_t dbg,
+									      uint32_t tag)
 {
 	const int ph = PH;
 	uint32_t t = blockIdx.x;
@@ -169,6 +173,7 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 	dsb_rflags_t f;
 	dsb_state_load(&w, &f, sp);
 	w.dbg = dbg;
+	w.launch_tag = tag;
 	uint64_t st[DSB_ST_N];
 	if (STATS) {
 		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
@@ -233,5 +238,6 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 
 /* launch signature shared by the lane (k_phase) and wave (k_wave_phase) phase kernels */
 typedef void (*dsb_phase_fn)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
-			     const uint32_t *, uint32_t, dsb_read_out_t *, uint32_t *, unsigned long long *, uint32_t);
+			     const uint32_t *, uint32_t, dsb_read_out_t *, uint32_t *, unsigned long long *, uint32_t,
+			     uint32_t);
 #endif

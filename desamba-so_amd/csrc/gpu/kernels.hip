@@ -229,8 +229,8 @@ struct dsb_gpu_dev {
 	dsb_dindex_t h;          /* host copy holding device pointers */
 	dsb_dindex_t *d;         /* device copy */
 	std::vector<void *> allocs;
-	dbuf ws_off, scale, ws, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2, woA, woB;
-	uint32_t epoch = 0;      /* run counter tagging the seeding sp_set slots (dsb_dindex_t.run_epoch) */
+	dbuf ws_off, scale, ws, wsr, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2, woA, woB;
+	uint32_t tag = 0;        /* phase-launch counter: the seeding sp_set slot tags (dsb_hset_tag) */
 };
 
 template <typename T>
@@ -335,7 +335,7 @@ extern "C" void dsb_gpu_free(dsb_index *ix)
 	hipSetDevice(g->device);
 	for (void *p : g->allocs)
 		hipFree(p);
-	dbuf *bs[] = {&g->ws_off, &g->scale, &g->ws, &g->order, &g->word_off, &g->ro, &g->mrl, &g->hits,
+	dbuf *bs[] = {&g->ws_off, &g->scale, &g->ws, &g->wsr, &g->order, &g->word_off, &g->ro, &g->mrl, &g->hits,
 		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2, &g->woA, &g->woB};
 	for (dbuf *b : bs)
 		b->release();
@@ -398,7 +398,7 @@ static size_t ws_budget(const dsb_gpu_dev *g)
 	size_t fr = 0, tot = 0;
 	if (hipMemGetInfo(&fr, &tot) != hipSuccess)
 		return (size_t)8 << 30;
-	size_t b = (size_t)((double)(fr + g->ws.cap) * 0.6); /* + 1/4 reserved for overflow re-runs */
+	size_t b = (size_t)((double)(fr + g->ws.cap) * 0.7); /* the rest: overflow re-runs (retry buffer), streams */
 	size_t cap = (size_t)200 << 30;
 	return b < cap ? b : cap;
 }
@@ -457,14 +457,23 @@ static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl,
 		abort();
 	}
 	uint32_t dbg = wave_dbg();
+	/* every launch gets its own slot tag; if the 32-bit counter ever wraps, the workspace is
+	 * cleared once (both streams drained) so that no slot of an earlier launch can match */
+	if (++g->tag == 0) {
+		hipDeviceSynchronize();
+		g->tag = 1;
+		if (g->ws.p)
+			hipMemset(g->ws.p, 0, g->ws.cap);
+	}
+	uint32_t tag = g->tag;
 	if (wave)
 		hipLaunchKernelGGL(fn, dim3(m), dim3(64), (ph == DSB_PH_DELA && (dbg & 512)) ? DSB_DELA_LDS : 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
-				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), dbg);
+				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), dbg, tag);
 	else
 		hipLaunchKernelGGL(fn, dim3(((ph == DSB_PH_ISLAND ? 2 : 1) * m + 63) / 64), dim3(64), 0, s, g->d, cl, g->ws_off.as<uint64_t>(),
 				   g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(), g->cnt.as<uint32_t>(),
-				   g->stats.as<unsigned long long>(), dbg);
+				   g->stats.as<unsigned long long>(), dbg, tag);
 }
 
 /* a batch of reads resident in HBM (sequences only) + its results */
@@ -475,6 +484,7 @@ struct dsb_gpu_batch {
 	dbuf seq, d_seq_off, d_len;
 	std::vector<dsb_read_out_t> ro;
 	std::vector<dsb_hit_out_t> hits;
+	std::vector<int32_t> carry; /* max_read_l each read's part B used (src/cly.c:2953) */
 };
 
 static int batch_upload(dsb_gpu_dev *g, const dsb_reads_t *reads, dsb_gpu_batch *b, dsb_gpu_timing &T, char *err,
@@ -633,24 +643,13 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	std::vector<uint32_t> scale(n, 1);
 	std::vector<uint64_t> ws_off(n);
 	std::vector<dsb_read_out_t> h_ro(n);
-	std::vector<int32_t> mrl(n);
+	std::vector<int32_t> &mrl = b->carry;
+	mrl.assign(n, 0);
 	std::vector<uint32_t> hit_off(n);
 	std::vector<uint64_t> word_off;
 	dsb_read_out_t *ro = b->ro.data();
 	std::vector<dsb_hit_out_t> &hv = b->hits;
 	size_t budget = ws_budget(g);
-	/* a new run epoch: seeding sp_set slots written by earlier runs never match this run's tags;
-	 * if the 32-bit epoch ever wraps, the workspace is cleared once so no old tag can repeat */
-	g->epoch++;
-	if (g->epoch == 0) {
-		g->epoch = 1;
-		if (g->ws.p)
-			HIP_OK(hipMemsetAsync(g->ws.p, 0, g->ws.cap, s));
-	}
-	{
-		uint32_t ep = g->epoch;
-		HIP_OK(hipMemcpy(&g->d->run_epoch, &ep, 4, hipMemcpyHostToDevice));
-	}
 	int carry = *max_read_l;
 	int l_ek = ix->l_ek;
 	for (uint64_t cb = 0; cb < n;) {
@@ -666,7 +665,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		}
 		uint32_t cn = (uint32_t)(ce - cb);
 		T.n_chunks++;
-		if (g->ws.ensure(ws_total + ws_total / 4 + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
+		uint64_t rused = 0; /* bytes of the retry buffer holding this chunk's re-run reads */
+		if (g->ws.ensure(ws_total + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
 		    g->word_off.ensure(8 * (size_t)cn + 16, err, errn))
 			return -1;
 		HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
@@ -772,22 +772,34 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 					snprintf(err, errn, "read %lu overflows every workspace size", (unsigned long)(cb + i));
 					return -1;
 				}
-				ws_off[cb + i] = ws_total + tot2;
+				ws_off[cb + i] = tot2; /* within this round's part of the retry buffer (rebased below) */
 				tot2 += dsb_layout(len[cb + i], dsb_default_caps(len[cb + i], scale[cb + i])).total;
 			}
-			if (ws_total + tot2 + 4096 <= g->ws.cap) { /* fits the reserve */
-				ws_total += tot2;
-			} else { /* grow the chunk workspace, keeping the first ws_total bytes */
+			/* the re-run reads live in a separate retry buffer (reads of earlier rounds keep their
+			 * bytes; growing it copies only those), addressed from the chunk's base pointer: a
+			 * read's offset is (retry buffer - chunk buffer) + its place there, modulo 2^64, so
+			 * every kernel keeps using ws + ws_off[r] and the chunk workspace is never duplicated */
+			if (rused + tot2 + 4096 > g->wsr.cap) {
 				void *np = nullptr;
-				size_t need = ws_total + tot2 + 4096;
+				size_t need = rused + tot2 + (rused + tot2) / 2 + 4096;
 				HIP_OK(hipMalloc(&np, need));
-				HIP_OK(hipMemcpyAsync(np, g->ws.p, ws_total, hipMemcpyDeviceToDevice, s));
+				if (rused)
+					HIP_OK(hipMemcpyAsync(np, g->wsr.p, rused, hipMemcpyDeviceToDevice, s));
 				HIP_OK(hipStreamSynchronize(s));
-				hipFree(g->ws.p);
-				g->ws.p = np;
-				g->ws.cap = need;
-				ws_total += tot2;
-				wsb = g->ws.as<uint8_t>();
+				uint64_t delta = (uint64_t)(uintptr_t)np - (uint64_t)(uintptr_t)g->wsr.p;
+				for (uint32_t i = 0; i < cn; i++) /* earlier retried reads move with the buffer */
+					if (scale[cb + i] > 1 && !std::binary_search(sel.begin(), sel.end(), i))
+						ws_off[cb + i] += delta;
+				if (g->wsr.p)
+					hipFree(g->wsr.p);
+				g->wsr.p = np;
+				g->wsr.cap = need;
+			}
+			{
+				uint64_t rbase = (uint64_t)(uintptr_t)g->wsr.p - (uint64_t)(uintptr_t)wsb + rused;
+				for (uint32_t i : sel)
+					ws_off[cb + i] += rbase;
+				rused += tot2;
 			}
 			HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
 			HIP_OK(hipMemcpyAsync(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
@@ -929,6 +941,7 @@ extern "C" int dsb_gpu_batch_run(dsb_index *ix, dsb_gpu_batch *b, int *max_read_
 
 extern "C" const dsb_read_out_t *dsb_gpu_batch_ro(const dsb_gpu_batch *b) { return b->ro.data(); }
 extern "C" const dsb_hit_out_t *dsb_gpu_batch_hits(const dsb_gpu_batch *b) { return b->hits.data(); }
+extern "C" const int32_t *dsb_gpu_batch_carry(const dsb_gpu_batch *b) { return b->carry.data(); }
 extern "C" uint64_t dsb_gpu_batch_n(const dsb_gpu_batch *b) { return b->n; }
 extern "C" uint64_t dsb_gpu_batch_bases(const dsb_gpu_batch *b) { return b->tot; }
 

@@ -68,6 +68,10 @@ def lib(path: str | None = None):
     L.dsb_batch_run.restype = C.c_int
     L.dsb_batch_format.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_void_p), u64p]
     L.dsb_batch_format.restype = C.c_int
+    L.dsb_batch_format_range.argtypes = [vp, vp, C.c_int, u64, u64, C.POINTER(C.c_void_p), u64p]
+    L.dsb_batch_format_range.restype = C.c_int
+    L.dsb_batch_carry.argtypes = [vp, C.c_void_p]
+    L.dsb_batch_carry.restype = C.c_int
     L.dsb_batch_taxa.argtypes = [vp, vp, C.c_int, C.c_void_p, C.c_void_p]
     L.dsb_batch_taxa.restype = C.c_int
     L.dsb_batch_reads.argtypes = [vp]
@@ -172,6 +176,19 @@ class Batch:
         out, n = C.c_void_p(), C.c_uint64(0)
         self.L.dsb_batch_format(self.ix.h, self.h, fmt, C.byref(out), C.byref(n))
         return _take(self.L, out, n.value)
+
+    def format_range(self, lo: int, hi: int, fmt: int = FMT_SAM) -> bytes:
+        """Records of reads [lo, hi) only."""
+        out, n = C.c_void_p(), C.c_uint64(0)
+        self.L.dsb_batch_format_range(self.ix.h, self.h, fmt, lo, hi, C.byref(out), C.byref(n))
+        return _take(self.L, out, n.value)
+
+    def carry(self):
+        """-> int32[n]: the max_read_l each read's length filter used in the last run."""
+        import numpy as np
+        c = np.zeros(self.n_reads, dtype=np.int32)
+        self.L.dsb_batch_carry(self.h, c.ctypes.data)
+        return c
 
     def taxa(self, flag: int = 0):
         """-> (tid uint32[n], weight uint64[n]) as meta_analysis assigns them."""

@@ -1,13 +1,22 @@
 """Multi-GPU sharding of the classify path (one process per GPU, torch.distributed).
 
-Reads shard across ranks with no data-path collective: each rank owns a contiguous block
-of FASTQ records, classifies it on its own GPU against its own replica of the index, and
-assigns one taxon per read exactly as meta_analysis does (reference src/cly_mt.c:902-961,
-dsb_batch_taxa).  The only exchange is the final per-taxon count reduction (all_reduce
-SUM over RCCL / "nccl"; "gloo" in the CPU tests), i.e. the node_count table of
-meta_analysis (src/cly_mt.c:1352-1362) for the whole input.
+Reads shard across ranks: each rank owns a contiguous block of FASTQ records, classifies it
+on its own GPU against its own replica of the index, and assigns one taxon per read exactly as
+meta_analysis does (reference src/cly_mt.c:902-961, dsb_batch_taxa).  Two exchanges:
+
+* the carried buffer-pool length (Classify_buff_pool.max_read_l, reference src/cly.c:2953):
+  a whole-input run carries the longest read that reached the length filter into every later
+  read.  Each rank publishes its own maximum (one int per rank, all_gather); a rank whose
+  earlier ranks reached the 2G-read threshold re-runs the leading reads whose own carry was
+  still below it (src/cly.c:2954 is the only place the carry is read, and only through
+  "max_read_l < 510", so no other read can change);
+* the final per-taxon count reduction (all_reduce SUM over RCCL / "nccl"; "gloo" in the CPU
+  tests): the node_count table of meta_analysis (src/cly_mt.c:1352-1362) for the whole input.
 """
 from __future__ import annotations
+
+# delete_small_score_rst's 2G-read branch (reference src/cly.c:2954: max_read_l < 510)
+CARRY_THRESHOLD = 510
 
 
 def shard_bounds(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -36,6 +45,33 @@ def split_fastq(data: bytes, rank: int, world: int) -> bytes:
     return data[offs[lo]:offs[hi]]
 
 
+def earlier_carry(local_carry: int, rank: int, world: int) -> int:
+    """Exclusive prefix max over ranks of their out-carry (all_gather of one int per rank)."""
+    import torch
+    import torch.distributed as dist
+    if world <= 1 or not (dist.is_available() and dist.is_initialized()):
+        return 0
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.zeros(world, dtype=torch.int64, device=dev)
+    t[rank] = int(local_carry)
+    dist.all_reduce(t)  # each slot written by exactly one rank: the reduce is a gather
+    return int(t[:rank].max().item()) if rank > 0 else 0
+
+
+def carry_rerun_prefix(carry, p_earlier: int) -> int:
+    """Reads to re-run once the carry of earlier ranks is known: the leading reads whose own
+    carry stayed below the 2G threshold while the earlier ranks' carry reached it.  carry is
+    monotone (a prefix max), so they form a prefix of the shard."""
+    if p_earlier < CARRY_THRESHOLD:
+        return 0  # max(p, c) < 510 exactly when c < 510: nothing the filter reads changes
+    k = 0
+    for c in carry:
+        if c >= CARRY_THRESHOLD:
+            break
+        k += 1
+    return k
+
+
 def taxon_counts(tid, weight, n_tax: int):
     """Per-taxon weights of one shard (meta_analysis node_count, src/cly_mt.c:1352-1362)."""
     import numpy as np
@@ -53,11 +89,45 @@ def reduce_counts(counts, device="cpu"):
     return t
 
 
-def classify_shard(index, data: bytes, rank: int, world: int, flag: int = 0, device="cuda"):
-    """Classify this rank's share of data on its GPU and return (global per-taxon counts,
-    this rank's batch).  index: a pydesamba.Index resident on this rank's GPU."""
+class ShardResult:
+    """One rank's classified share: the batch, plus the re-run of its leading reads when the
+    carry of earlier ranks changed them (prefix reads come from `head`)."""
+
+    def __init__(self, batch, head=None, k: int = 0):
+        self.batch, self.head, self.k = batch, head, k
+
+    def taxa(self, flag: int = 0):
+        tid, w = self.batch.taxa(flag)
+        if self.head is not None:
+            ht, hw = self.head.taxa(flag)
+            tid[:self.k], w[:self.k] = ht, hw
+        return tid, w
+
+    def format(self, fmt: int = 1) -> bytes:
+        if self.head is None:
+            return self.batch.format(fmt)
+        return self.head.format(fmt) + self.batch.format_range(self.k, self.batch.n_reads, fmt)
+
+    def close(self):
+        for b in (self.head, self.batch):
+            if b is not None:
+                b.close()
+
+
+def classify_shard(index, data: bytes, rank: int, world: int, flag: int = 0, device="cuda", carry_in: int = 0):
+    """Classify this rank's share of data on its GPU; returns (global per-taxon counts,
+    ShardResult).  index: a pydesamba.Index resident on this rank's GPU.  The result equals
+    one whole-input read_classify call (carry_in: that call's incoming max_read_l)."""
     part = split_fastq(data, rank, world)
     batch = index.batch(part)
-    batch.run(max_read_l=0)
-    tid, w = batch.taxa(flag)
-    return reduce_counts(taxon_counts(tid, w, index.max_tid() + 1), device), batch
+    batch.run(max_read_l=carry_in)
+    p = max(carry_in, earlier_carry(batch.max_read_l, rank, world))
+    res = ShardResult(batch)
+    k = carry_rerun_prefix(batch.carry(), p) if batch.n_reads else 0
+    if k:
+        offs = fastq_records(part)
+        head = index.batch(part[:offs[k]])
+        head.run(max_read_l=p)
+        res = ShardResult(batch, head, k)
+    tid, w = res.taxa(flag)
+    return reduce_counts(taxon_counts(tid, w, index.max_tid() + 1), device), res

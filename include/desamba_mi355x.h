@@ -35,6 +35,12 @@ typedef struct dsb_batch dsb_batch;
 dsb_batch *dsb_batch_create(void *idx, const char *text, uint64_t text_n, dsb_timing_t *timing);
 int dsb_batch_run(void *idx, dsb_batch *b, int *max_read_l, dsb_timing_t *timing);
 int dsb_batch_format(void *idx, dsb_batch *b, int format, char **output, uint64_t *output_n);
+/* the records of reads [lo, hi) only (input order), as dsb_batch_format writes them */
+int dsb_batch_format_range(void *idx, dsb_batch *b, int format, uint64_t lo, uint64_t hi, char **output,
+			   uint64_t *output_n);
+/* carry_out[i] = the max_read_l read i's length filter used in the last run (the carried
+ * Classify_buff_pool.max_read_l, reference src/cly.c:2953-2963); monotone over the batch */
+int dsb_batch_carry(dsb_batch *b, int32_t *carry_out);
 /* Per-read taxon as meta_analysis assigns it (ana_get_tid, reference src/cly_mt.c:902-961):
  * tid_out[i] (0 = unclassified); weight_out[i] = 1 or the read length (flag & 1). */
 int dsb_batch_taxa(void *idx, dsb_batch *b, int flag, uint32_t *tid_out, uint64_t *weight_out);

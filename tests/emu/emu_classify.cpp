@@ -103,14 +103,17 @@ int main(int argc, char **argv)
 			}
 			if (getenv("EMU_WAVE")) { /* the wave-cooperative code paths, as a one-lane wave */
 				dsb_rflags_t f = {0, 0, 0, 0};
-				uint64_t *hset = (uint64_t *)(arena.data() + lay.hset);
+				/* one sp_set table for all reads, never cleared, as the GPU reuses workspace bytes
+				 * across launches and chunks: only the per-launch slot tags keep it exact */
+				static std::vector<uint64_t> hset_store(DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS * 64, 0);
+				static uint32_t launch_tag = 0;
+				uint64_t *hset = hset_store.data();
 				for (int ph = 0; ph < DSB_PH_DELA; ph++) {
+					w.launch_tag = ++launch_tag;
 					if ((ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) && dsb_phase_active(&w, &f, ph)) {
-						memset(hset, 0, 8ull * DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS * 64);
 						static int32_t sm_lds[2];
 						dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, sm_lds);
 					} else if ((ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) && dsb_phase_active(&w, &f, ph)) {
-						memset(hset, 0, 8ull * DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS * 64);
 						static int32_t sm_lds2[2];
 						dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem, sm_lds2);
 					} else

@@ -165,3 +165,23 @@ def test_dlopen_consumer_example(fixture_index, tmp_path):
     assert r.stdout == golden("mixed.herm.sam_full")
     ref_lines = golden("mixed.meta_reads").decode().splitlines()
     assert r.stderr.decode().endswith("\n".join(l for l in ref_lines if not l.startswith("#")) + "\n")
+
+
+@pytest.mark.parametrize("budget_mb", ["48", "4"])
+def test_many_chunks_and_second_strand_passes_byte_identical(gpu_index, pyd, budget_mb):
+    """A small workspace budget splits the reads into many chunks that reuse the same workspace
+    bytes (the seeding sp_set tables are never cleared: only per-launch slot tags keep them
+    exact), and the both-strand reads run FAST1/SLOW1 over tables FAST0/SLOW0 just used."""
+    os.environ["DSB_WS_BUDGET_MB"] = budget_mb
+    try:
+        fast1 = slow1 = 0
+        for name in ("mixed", "ont", "ont_long"):
+            out, t, _ = gpu_index.classify(golden(name + ".fq"), fmt=pyd.FMT_SAM, stats=True)
+            assert t["n_chunks"] >= 3, (name, t["n_chunks"])
+            assert out == golden(name + ".herm.sam"), name
+            fast1 += t["stats_phase"]["fast1"]["mem_search"]
+            slow1 += t["stats_phase"]["slow1"]["mem_search"]
+        assert fast1 > 0
+        print(f"FAST1 MEM searches {fast1}, SLOW1 MEM searches {slow1}")
+    finally:
+        os.environ.pop("DSB_WS_BUDGET_MB", None)

@@ -67,3 +67,33 @@ def test_taxon_count_reduce_world2(fixture_index, world):
     for r in range(world):
         assert (res[r] == want).all()
     assert want.sum() == len(tids) and want[0] < len(tids)
+
+
+def test_carry_rerun_prefix_only_when_earlier_ranks_cross_the_2g_threshold():
+    # reference src/cly.c:2954: the carried max_read_l is only read through "< 510"
+    assert shard.carry_rerun_prefix([0, 150, 150, 600, 900], 509) == 0
+    assert shard.carry_rerun_prefix([0, 150, 150, 600, 900], 510) == 3
+    assert shard.carry_rerun_prefix([700, 900], 8000) == 0
+    assert shard.carry_rerun_prefix([150] * 7, 600) == 7
+    assert shard.carry_rerun_prefix([], 600) == 0
+
+
+def _carry_worker(rank, world, port, carries, q):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    q.put((rank, shard.earlier_carry(carries[rank], rank, world)))
+    dist.destroy_process_group()
+
+
+def test_earlier_carry_is_exclusive_prefix_max_world3():
+    carries = [300, 8000, 150]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_carry_worker, args=(r, 3, port, carries, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: 0, 1: 300, 2: 8000}
