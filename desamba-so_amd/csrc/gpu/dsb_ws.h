@@ -14,6 +14,7 @@
 #define DSB_BIN_TAIL 256   /* bytes after R, MALLOC_PERTURB fill */
 #define DSB_STATE_BYTES 128
 #define DSB_CAP_RETRY 8
+#define DSB_SCALE_UNIT 8   /* capacity scale is fixed point: DSB_SCALE_UNIT = the default capacities */
 
 DSB_HD uint64_t dsb_al(uint64_t x) { return (x + 255) & ~255ull; }
 
@@ -29,9 +30,9 @@ DSB_HD int dsb_key_len(uint32_t q_len) /* build_hash_table_M2, src/cly.c:2179-21
 DSB_HD dsb_caps_t dsb_default_caps(uint32_t L, uint32_t scale)
 {
 	dsb_caps_t c;
-	c.anc = (1024 + (L >> 2)) * scale;
+	c.anc = (uint32_t)(((uint64_t)(1024 + (L >> 2)) * scale) / DSB_SCALE_UNIT);
 	c.hit = c.anc;
-	c.sms = (2048 + (L >> 1)) * scale;
+	c.sms = (uint32_t)(((uint64_t)(2048 + (L >> 1)) * scale) / DSB_SCALE_UNIT);
 	return c;
 }
 

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ i
 	uint32_t word = (uint32_t)(strand ? wi - nw : wi);
 	uint8_t *base = ws + ws_off[r];
 	const uint8_t *bin = base + DSB_BIN_GUARD + strand * L;
-	dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, 1)); /* ex offsets do not depend on caps */
+	dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, DSB_SCALE_UNIT)); /* ex offsets do not depend on caps */
 	uint64_t *ex = (uint64_t *)(base + (strand ? lay.exR : lay.exF));
 	uint32_t *pre = (uint32_t *)(base + lay.pre) + (strand ? L : 0);
 	uint32_t k = word * 64 + lane;
@@ -640,7 +640,12 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	    g->cnt.ensure(64, err, errn) || g->stats.ensure(8 * DSB_N_STATS, err, errn) || g->ws_off.ensure(8 * n + 8, err, errn))
 		return -1;
 	HIP_OK(hipMemsetAsync(g->stats.p, 0, 8 * DSB_N_STATS, s));
-	std::vector<uint32_t> scale(n, 1);
+	/* DSB_TEST_SCALE0 (tests): start below the default capacities so that reads overflow and
+	 * take the re-run path */
+	uint32_t scale0 = DSB_SCALE_UNIT;
+	if (const char *e = getenv("DSB_TEST_SCALE0"))
+		scale0 = (uint32_t)DSB_MAX(1, atoi(e));
+	std::vector<uint32_t> scale(n, scale0);
 	std::vector<uint64_t> ws_off(n);
 	std::vector<dsb_read_out_t> h_ro(n);
 	std::vector<int32_t> &mrl = b->carry;
@@ -656,7 +661,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		/* ---- chunk [cb, ce) within the workspace budget, input order */
 		uint64_t ce = cb, ws_total = 0;
 		while (ce < n) {
-			uint64_t sz = dsb_layout(len[ce], dsb_default_caps(len[ce], 1)).total;
+			uint64_t sz = dsb_layout(len[ce], dsb_default_caps(len[ce], scale[ce])).total;
 			if (ce > cb && ws_total + sz > budget)
 				break;
 			ws_off[ce] = ws_total;
@@ -756,6 +761,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			}
 		}
 		HIP_OK(hipGetLastError());
+		HIP_OK(hipStreamSynchronize(s));
 		uint32_t n_over = 0;
 		HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
 		HIP_OK(hipMemcpy(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
@@ -768,7 +774,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			uint64_t tot2 = 0;
 			for (uint32_t i : sel) {
 				scale[cb + i] *= DSB_CAP_RETRY;
-				if (scale[cb + i] > 4096) {
+				if (scale[cb + i] > 4096 * DSB_SCALE_UNIT) {
 					snprintf(err, errn, "read %lu overflows every workspace size", (unsigned long)(cb + i));
 					return -1;
 				}
@@ -788,7 +794,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				HIP_OK(hipStreamSynchronize(s));
 				uint64_t delta = (uint64_t)(uintptr_t)np - (uint64_t)(uintptr_t)g->wsr.p;
 				for (uint32_t i = 0; i < cn; i++) /* earlier retried reads move with the buffer */
-					if (scale[cb + i] > 1 && !std::binary_search(sel.begin(), sel.end(), i))
+					if (scale[cb + i] > scale0 && !std::binary_search(sel.begin(), sel.end(), i))
 						ws_off[cb + i] += delta;
 				if (g->wsr.p)
 					hipFree(g->wsr.p);
@@ -822,6 +828,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			for (int ph = 0; ph < DSB_PH_N; ph++)
 				launch_phase(g, ph, false, cl, wsb, g->sel.as<uint32_t>(), m);
 			HIP_OK(hipGetLastError());
+			/* the re-run went to the non-blocking stream: drain it before the (null-stream) copies */
+			HIP_OK(hipStreamSynchronize(s));
 			HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
 			HIP_OK(hipMemcpy(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
 		}

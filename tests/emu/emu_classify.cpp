@@ -67,7 +67,7 @@ int main(int argc, char **argv)
 		uint32_t L = reads.rec[i].seq_l;
 		const uint8_t *seq = (const uint8_t *)reads.arena + reads.rec[i].seq_off;
 		dsb_read_out_t ro;
-		for (uint32_t scale = 1;; scale *= DSB_CAP_RETRY) {
+		for (uint32_t scale = DSB_SCALE_UNIT;; scale *= DSB_CAP_RETRY) {
 			dsb_caps_t cap = dsb_default_caps(L, scale);
 			dsb_ws_layout lay = dsb_layout(L, cap);
 			arena.assign(lay.total + 256, (uint8_t)(getenv("EMU_FILL") ? strtol(getenv("EMU_FILL"), 0, 0) : 0xEE));

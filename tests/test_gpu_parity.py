@@ -167,21 +167,70 @@ def test_dlopen_consumer_example(fixture_index, tmp_path):
     assert r.stderr.decode().endswith("\n".join(l for l in ref_lines if not l.startswith("#")) + "\n")
 
 
+def _chimeras(n):
+    """Reads that match both strands about equally (a forward half + the reverse complement of
+    another read's half), so that classify_seq takes the both_direction branch (FAST1, SLOW1)."""
+    comp = bytes.maketrans(b"ACGTN", b"TGCAN")
+    lines = golden("ont.fq").split(b"\n")
+    seqs = [lines[i + 1] for i in range(0, len(lines) - 3, 4)]
+    out = []
+    for k in range(n):
+        a, b = seqs[(2 * k) % len(seqs)], seqs[(2 * k + 1) % len(seqs)]
+        h = min(len(a), len(b)) // 2
+        s = a[:h] + b[:h].translate(comp)[::-1]
+        out.append(b"@chim%d\n%s\n+\n%s\n" % (k, s, b"I" * len(s)))
+    return b"".join(out)
+
+
 @pytest.mark.parametrize("budget_mb", ["48", "4"])
-def test_many_chunks_and_second_strand_passes_byte_identical(gpu_index, pyd, budget_mb):
+def test_many_chunks_and_second_strand_passes_byte_identical(gpu_index, fixture_index, pyd, budget_mb, tmp_path):
     """A small workspace budget splits the reads into many chunks that reuse the same workspace
     bytes (the seeding sp_set tables are never cleared: only per-launch slot tags keep them
-    exact), and the both-strand reads run FAST1/SLOW1 over tables FAST0/SLOW0 just used."""
+    exact), and reads matching both strands run FAST1/SLOW1 over the tables FAST0/SLOW0 just
+    used.  Goldens: the committed hermetic outputs, and the hermetic reference run on this box
+    for the chimeric reads."""
+    herm = os.path.join(ROOT, "oracle", "_ref", "herm_classify")
+    if not os.path.exists(herm):
+        pytest.skip("oracle/_ref not built")
+    chim = _chimeras(400)
+    fq = tmp_path / "chim.fq"
+    fq.write_bytes(chim)
+    chim_ref = subprocess.run([herm, "--sam", fixture_index, str(fq)], capture_output=True, check=True,
+                              timeout=300).stdout
     os.environ["DSB_WS_BUDGET_MB"] = budget_mb
     try:
         fast1 = slow1 = 0
-        for name in ("mixed", "ont", "ont_long"):
-            out, t, _ = gpu_index.classify(golden(name + ".fq"), fmt=pyd.FMT_SAM, stats=True)
+        for name, data, ref in [("mixed", golden("mixed.fq"), golden("mixed.herm.sam")),
+                                ("ont_long", golden("ont_long.fq"), golden("ont_long.herm.sam")),
+                                ("chimeras", chim, chim_ref)]:
+            out, t, _ = gpu_index.classify(data, fmt=pyd.FMT_SAM, stats=True)
             assert t["n_chunks"] >= 3, (name, t["n_chunks"])
-            assert out == golden(name + ".herm.sam"), name
+            r = compare(ref, out)
+            assert r["full_mismatch"] == 0, (name, r)
+            assert out == ref, name
             fast1 += t["stats_phase"]["fast1"]["mem_search"]
             slow1 += t["stats_phase"]["slow1"]["mem_search"]
         assert fast1 > 0
         print(f"FAST1 MEM searches {fast1}, SLOW1 MEM searches {slow1}")
     finally:
+        os.environ.pop("DSB_WS_BUDGET_MB", None)
+
+
+def test_overflow_reruns_byte_identical(gpu_index, pyd):
+    """Every read starts at 1/8 of the default workspace capacities (DSB_TEST_SCALE0=1), so many
+    overflow and are re-run with larger capacities in the retry buffer (several rounds, and with
+    a small budget several chunks): still byte-identical to the hermetic reference."""
+    os.environ["DSB_TEST_SCALE0"] = "1"
+    try:
+        for budget in (None, "8"):
+            if budget:
+                os.environ["DSB_WS_BUDGET_MB"] = budget
+            retried = 0
+            for name in ("mixed", "ont", "ont_long"):
+                out, t, _ = gpu_index.classify(golden(name + ".fq"), fmt=pyd.FMT_SAM)
+                retried += t["n_retry"]
+                assert out == golden(name + ".herm.sam"), (name, budget)
+            assert retried > 0
+    finally:
+        os.environ.pop("DSB_TEST_SCALE0", None)
         os.environ.pop("DSB_WS_BUDGET_MB", None)
