@@ -546,50 +546,53 @@ DSB_HD uint32_t dsb_get_uni_w(dsb_read_ws *w, uint64_t bwt_pos, int search_l, ui
 	return u;
 }
 
-/* dst[0..32) = src[0..32) (word loads) */
-DSB_HD void dsb_copy32(uint8_t *dst, const uint8_t *src)
+/* bytes k = 0..15 of lo | hi = end[-k] (two word loads; the read buffer has guards) */
+DSB_HD void dsb_rev16(const uint8_t *end, uint64_t *lo, uint64_t *hi)
 {
-	for (int k = 0; k < 4; k++) {
-		uint64_t v = dsb_ld8u(src + 8 * k);
-		for (int b = 0; b < 8; b++)
-			dst[8 * k + b] = (uint8_t)(v >> (8 * b));
-	}
+	*lo = __builtin_bswap64(dsb_ld8u(end - 7));
+	*hi = __builtin_bswap64(dsb_ld8u(end - 15));
 }
 
-/* dst[k] = end[-k] for k < n (n <= 16), from two word loads (the read buffer has guards) */
-DSB_HD void dsb_rev_copy(uint8_t *dst, const uint8_t *end, uint32_t n)
+/* get_ref of <= 16 bases into string bytes [0, length) of a register window */
+DSB_HD void dsb_get_ref_r(dsb_read_ws *w, dsb_w32 &T, uint64_t uni_offset, uint32_t length, int isForward)
 {
-	uint64_t a = dsb_ld8u(end - 7), b = dsb_ld8u(end - 15);
-	for (uint32_t k = 0; k < n; k++)
-		dst[k] = (uint8_t)((k < 8 ? (a >> (8 * (7 - k))) : (b >> (8 * (15 - k)))) & 0xff);
+	if (w->stats) w->stats[DSB_ST_GETREF_B] += (length + 3) / 4;
+	uint64_t lo, hi;
+	dsb_get_ref16(w->ix, uni_offset, length, isForward, &lo, &hi);
+	dsb_w32_put(T, length, lo, hi);
 }
 
-/* get_new_ed, src/cly.c:624-689 */
+/* get_new_ed, src/cly.c:624-689.  q_buff / t_buff (32-byte stack buffers, pattern-initialised)
+ * are register windows; the query of the reverse direction is read in place (two word loads
+ * per step), as the reference compares against the read buffer itself. */
 DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t *len_, uint32_t *l_mem_ext,
 			    int32_t q_off, uint64_t t_off, uint32_t l_read, int is_FWD)
 {
-	uint8_t qbuf[32], tbuf[32];
-	for (int k = 0; k < 32; k++) { qbuf[k] = DSB_STACK_PATTERN; tbuf[k] = DSB_STACK_PATTERN; }
-	uint8_t *q = qbuf + 8, *t = tbuf + 8;
+	dsb_w32 Q = dsb_w32_splat(DSB_STACK_PATTERN), T = Q;
+	const uint8_t *q = q_b;
 	uint32_t len, max_len;
+	uint64_t lo, hi, ql, qh;
 	if (is_FWD) {
 		if (q_off < 0)
 			q_off = 0;
 		max_len = q_off;
 		len = DSB_MIN(12u, max_len);
-		dsb_rev_copy(q, q_b + q_off, len);
+		dsb_rev16(q_b + q_off, &lo, &hi);
+		dsb_w32_put(Q, len, lo, hi);
+		ql = Q.b;
+		qh = Q.c;
 	} else {
 		max_len = l_read - q_off;
 		len = DSB_MIN(12u, max_len);
 		q = q_b + q_off;
+		ql = dsb_ld8u(q);
+		qh = dsb_ld8u(q + 8);
 	}
-	dsb_get_ref_w(w, t, t_off, len, !is_FWD);
-	if (len > 0 && t[0] == q[0]) {
-		int mtc;
+	dsb_get_ref_r(w, T, t_off, len, !is_FWD);
+	if (len > 0 && (T.b & 0xff) == (ql & 0xff)) {
+		uint32_t mtc;
 		do {
-			for (mtc = 0; mtc < (int)len; mtc++)
-				if (t[mtc] != q[mtc])
-					break;
+			mtc = dsb_w32_mismatch(T, ql, qh, len); /* for (mtc = 0; mtc < len; mtc++) if (t[mtc] != q[mtc]) break; */
 			if (mtc > 0) {
 				*l_mem_ext += mtc;
 				max_len -= mtc;
@@ -597,20 +600,23 @@ DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t
 				if (is_FWD) {
 					q_off -= mtc;
 					t_off -= mtc;
-					dsb_rev_copy(q, q_b + q_off, len);
+					dsb_rev16(q_b + q_off, &lo, &hi);
+					dsb_w32_put(Q, len, lo, hi);
+					ql = Q.b;
+					qh = Q.c;
 				} else {
 					t_off += mtc;
 					q += mtc;
+					ql = dsb_ld8u(q);
+					qh = dsb_ld8u(q + 8);
 				}
-				dsb_get_ref_w(w, t, t_off, len, !is_FWD);
+				dsb_get_ref_r(w, T, t_off, len, !is_FWD);
 			}
 		} while (mtc > 0);
 	}
-	if (!is_FWD) { /* lv_extd writes its terminator at q[len]: work on a private copy (lanes share the read) */
-		dsb_copy32(qbuf, q - 8);
-		q = qbuf + 8;
-	}
-	*e_d = dsb_lv_extd_w(t, len, q, len);
+	if (!is_FWD) /* lv_extd terminates a copy of the read's bytes (q - 8 .. q + 24) */
+		Q = dsb_w32_load(q - 8);
+	*e_d = (uint32_t)dsb_lv_extd_r(T, (int32_t)len, Q, (int32_t)len);
 	*len_ = len;
 }
 
@@ -664,14 +670,14 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 	uint32_t l_pre = 0, l_suf = 0;
 	uint32_t d_pre = 0, d_suf = 0;
 	int32_t s = 0, max_s = 0;
-	/* stack windows of the reference: q_pre/t_pre/t_suf[LV_L + 1] */
-	uint8_t qpre_b[32], tpre_b[32], tsuf_b[32];
-	for (int k = 0; k < 32; k++) { qpre_b[k] = DSB_STACK_PATTERN; tpre_b[k] = DSB_STACK_PATTERN; tsuf_b[k] = DSB_STACK_PATTERN; }
-	uint8_t *q_pre = qpre_b + 8, *t_pre = tpre_b + 8, *t_suf = tsuf_b + 8;
+	/* stack windows q_pre / t_pre / t_suf[LV_L + 1] (src/cly.c:705-707), in registers */
+	dsb_w32 QP = dsb_w32_splat(DSB_STACK_PATTERN), TP = QP, TS = QP;
+	uint64_t lo, hi;
 	do {
-		uint8_t *q_suf;
+		const uint8_t *q_suf;
 		l_pre = DSB_MIN(q_off + 1, DSB_LV_L);
-		dsb_rev_copy(q_pre, q_b + q_off, l_pre);
+		dsb_rev16(q_b + q_off, &lo, &hi);
+		dsb_w32_put(QP, l_pre, lo, hi);
 		int s_l = 0;
 		if (m_r->sa_sp != ~0ull) {
 			uni = (int32_t)dsb_get_uni_w(w, m_r->sa_sp, m_r->sa_sp_l, &t_off, &u_off);
@@ -684,7 +690,7 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 				new_sp = dsb_lf_w(w, b_p, &c);
 				if (c == 4)
 					break;
-				t_pre[s_l++] = c;
+				dsb_w32_set_byte(TP, s_l++, c);
 				b_p = new_sp;
 				if ((uint32_t)s_l >= l_pre)
 					break;
@@ -698,9 +704,9 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 			if (ix->uni[uni].length < DSB_MIN_UNI_L)
 				break;
 			l_pre = DSB_MIN(l_pre, u_off);
-			dsb_get_ref_w(w, t_pre, t_off - 1, l_pre, 0);
+			dsb_get_ref_r(w, TP, t_off - 1, l_pre, 0);
 		}
-		d_pre = dsb_lv_extd_w(t_pre, l_pre, q_pre, l_pre);
+		d_pre = dsb_lv_extd_r(TP, l_pre, QP, l_pre);
 		s = dsb_qmem(ix, l_m) + Q_LV[d_pre * DSB_LV_DIM + l_pre];
 		if (s < DSB_MIN_S_1 && l_pre == DSB_LV_L && uni < 0) {
 			s = 0;
@@ -723,26 +729,26 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 		if (l_max_suf != 0) {
 			l_suf = DSB_MIN(l_max_suf, (uint32_t)DSB_LV_L);
 			q_suf = q_b + q_off_r;
-			dsb_get_ref_w(w, t_suf, t_off + l_m, l_suf, 1);
-			if (t_suf[0] == q_suf[0]) {
-				int mtc;
+			uint64_t ql = dsb_ld8u(q_suf), qh = dsb_ld8u(q_suf + 8);
+			dsb_get_ref_r(w, TS, t_off + l_m, l_suf, 1);
+			if ((TS.b & 0xff) == (ql & 0xff)) {
+				uint32_t mtc;
 				do {
-					for (mtc = 0; mtc < (int)l_suf; mtc++)
-						if (t_suf[mtc] != q_suf[mtc])
-							break;
+					mtc = dsb_w32_mismatch(TS, ql, qh, l_suf);
 					if (mtc > 0) {
 						l_m += mtc;
 						s = dsb_qmem(ix, l_m) + Q_LV[d_pre * DSB_LV_DIM + l_pre];
 						l_max_suf -= mtc;
 						l_suf = DSB_MIN(l_max_suf, (uint32_t)DSB_LV_L);
 						q_suf += mtc;
-						dsb_get_ref_w(w, t_suf, t_off + l_m, l_suf, 1);
+						ql = dsb_ld8u(q_suf);
+						qh = dsb_ld8u(q_suf + 8);
+						dsb_get_ref_r(w, TS, t_off + l_m, l_suf, 1);
 					}
 				} while (mtc > 0);
 			}
-			uint8_t qsuf_b[32]; /* private copy: lv_extd writes its terminator at q_suf[l_suf] */
-			dsb_copy32(qsuf_b, q_suf - 8);
-			d_suf = dsb_lv_extd_w(t_suf, l_suf, qsuf_b + 8, l_suf);
+			/* lv_extd terminates a copy of the read's bytes (q_suf - 8 .. q_suf + 24) */
+			d_suf = dsb_lv_extd_r(TS, l_suf, dsb_w32_load(q_suf - 8), l_suf);
 			s += Q_LV[d_suf * DSB_LV_DIM + l_suf];
 		} else
 			l_suf = d_suf = 0;

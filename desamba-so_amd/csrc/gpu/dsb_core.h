@@ -392,61 +392,141 @@ DSB_HD int32_t dsb_lv_extd(uint8_t *ref, int32_t ref_length, uint8_t *query, int
 }
 
 /*
- * lv_extd on a 32-byte window held in registers: ref / query point 8 bytes into 32-byte buffers
- * (every caller's buffer), so the bytes the reference can touch, ref[-5 .. len+4]
- * and query[-1 .. len], are four u64 words each.  The terminators go into the register copies
- * (the caller's buffers are left as they are, as the reference restores them), and the in-line
- * match `for (; ref[mn + j] == query[mn]; mn++)` compares 8 bytes per step (first differing byte
- * of the XOR).  It always stops at query's '$' (ref holds no '$'), within the window.
- * Same result as dsb_lv_extd for every input of that shape (tests/test_lv_words.py).
+ * 32-byte stack buffers of the reference held in four registers.  Every lv_extd caller's
+ * windows are 32-byte buffers with the string at +8, so the bytes the reference
+ * can touch, ref[-5 .. len+4] and query[-1 .. len], are four u64 words: byte x of the string
+ * (x in [-8, 24)) is byte (x + 8) & 7 of word (x + 8) >> 3.  The accessors select words with
+ * masks instead of indexing an array: a dynamically indexed private array lives in scratch
+ * memory, and every byte compare of the map_seed / get_new_ed windows became a scratch load.
  */
-DSB_HD uint64_t dsb_win8(const uint64_t *W, int x) /* bytes x .. x+7 of the window, x in [-8, 16] */
+struct dsb_w32 { uint64_t a, b, c, d; };
+
+DSB_HD dsb_w32 dsb_w32_splat(uint8_t v)
+{
+	uint64_t p = 0x0101010101010101ull * v;
+	dsb_w32 W = {p, p, p, p};
+	return W;
+}
+/* the 32 bytes at buf (= string - 8) */
+DSB_HD dsb_w32 dsb_w32_load(const uint8_t *buf)
+{
+	dsb_w32 W = {dsb_ld8u(buf), dsb_ld8u(buf + 8), dsb_ld8u(buf + 16), dsb_ld8u(buf + 24)};
+	return W;
+}
+DSB_HD uint64_t dsb_w32_word(const dsb_w32 &W, int i) /* word i, 0 outside [0, 4) */
+{
+	return (W.a & (0ull - (uint64_t)(i == 0))) | (W.b & (0ull - (uint64_t)(i == 1))) |
+	       (W.c & (0ull - (uint64_t)(i == 2))) | (W.d & (0ull - (uint64_t)(i == 3)));
+}
+DSB_HD uint64_t dsb_w32_8(const dsb_w32 &W, int x) /* string bytes x .. x+7, x in [-8, 16]; past the buffer: 0 */
 {
 	int b = x + 8;
 	int i = b >> 3, sh = (b & 7) * 8;
-	uint64_t lo = W[0], hi = W[1];
-	if (i == 1) { lo = W[1]; hi = W[2]; }
-	if (i == 2) { lo = W[2]; hi = W[3]; }
-	if (i >= 3) { lo = W[3]; hi = 0; }
+	uint64_t lo = dsb_w32_word(W, i), hi = dsb_w32_word(W, i + 1);
 	return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
 }
-DSB_HD uint32_t dsb_byte_at(const uint64_t *W, int x)
+DSB_HD uint32_t dsb_w32_byte(const dsb_w32 &W, int x)
 {
 	int b = x + 8;
-	uint64_t w0 = W[0];
-	if ((b >> 3) == 1) w0 = W[1];
-	if ((b >> 3) == 2) w0 = W[2];
-	if ((b >> 3) >= 3) w0 = W[3];
-	return (uint32_t)(w0 >> ((b & 7) * 8)) & 0xff;
+	return (uint32_t)(dsb_w32_word(W, b >> 3) >> ((b & 7) * 8)) & 0xff;
 }
-DSB_HD void dsb_set_byte(uint64_t *W, int x, uint32_t v)
+DSB_HD void dsb_w32_set_byte(dsb_w32 &W, int x, uint32_t v)
 {
 	int b = x + 8;
-	uint64_t m = 0xffull << ((b & 7) * 8), val = (uint64_t)v << ((b & 7) * 8);
+	uint64_t m = 0xffull << ((b & 7) * 8), val = (uint64_t)(v & 0xff) << ((b & 7) * 8);
 	int i = b >> 3;
-	if (i == 0) W[0] = (W[0] & ~m) | val;
-	if (i == 1) W[1] = (W[1] & ~m) | val;
-	if (i == 2) W[2] = (W[2] & ~m) | val;
-	if (i == 3) W[3] = (W[3] & ~m) | val;
+	if (i == 0) W.a = (W.a & ~m) | val;
+	if (i == 1) W.b = (W.b & ~m) | val;
+	if (i == 2) W.c = (W.c & ~m) | val;
+	if (i == 3) W.d = (W.d & ~m) | val;
 }
-DSB_HD int32_t dsb_lv_extd_w(const uint8_t *ref_, int32_t ref_length, const uint8_t *query_, int32_t query_length)
+/* string bytes [0, n) := bytes of lo | hi (n <= 16); the bytes past n keep what they held */
+DSB_HD void dsb_w32_put(dsb_w32 &W, uint32_t n, uint64_t lo, uint64_t hi)
 {
-	uint64_t R[4], Q[4];
-	for (int k = 0; k < 4; k++) {
-		uint64_t a = 0, b = 0;
-		for (int e = 0; e < 8; e++) {
-			a |= (uint64_t)ref_[8 * k + e - 8] << (8 * e);
-			b |= (uint64_t)query_[8 * k + e - 8] << (8 * e);
+	uint64_t m1 = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+	uint32_t n2 = n > 8 ? n - 8 : 0;
+	uint64_t m2 = n2 >= 8 ? ~0ull : ((1ull << (8 * n2)) - 1);
+	W.b = (W.b & ~m1) | (lo & m1);
+	W.c = (W.c & ~m2) | (hi & m2);
+}
+/* first k < n (n <= 16) with string byte k of T != byte k of (q_lo | q_hi); n if none */
+DSB_HD uint32_t dsb_w32_mismatch(const dsb_w32 &T, uint64_t q_lo, uint64_t q_hi, uint32_t n)
+{
+	uint64_t m1 = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+	uint32_t n2 = n > 8 ? n - 8 : 0;
+	uint64_t m2 = n2 >= 8 ? ~0ull : ((1ull << (8 * n2)) - 1);
+	uint64_t x1 = (T.b ^ q_lo) & m1, x2 = (T.c ^ q_hi) & m2;
+	if (x1)
+		return (uint32_t)__builtin_ctzll(x1) >> 3;
+	if (x2)
+		return 8 + ((uint32_t)__builtin_ctzll(x2) >> 3);
+	return n;
+}
+
+/* get_ref (above) of length <= 16 bases as bytes k = 0 .. length-1 of lo | hi */
+DSB_HD void dsb_get_ref16(const dsb_dindex_t *ix, uint64_t uni_offset, uint32_t length, int isForward, uint64_t *lo_,
+			  uint64_t *hi_)
+{
+	uint64_t lo = 0, hi = 0;
+	if (isForward) {
+		uint64_t B = uni_offset >> 2;
+		if (B + 16 <= ix->ref_bin_padded) {
+			uint64_t y = __builtin_bswap64(dsb_ld8u(ix->ref_bin + B)) << (2 * (uint32_t)(uni_offset & 3));
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+			for (int k = 0; k < 8; k++) {
+				lo |= ((y >> (62 - 2 * k)) & 3) << (8 * k);
+				hi |= ((y >> (46 - 2 * k)) & 3) << (8 * k);
+			}
+			*lo_ = lo;
+			*hi_ = hi;
+			return;
 		}
-		R[k] = a;
-		Q[k] = b;
+	} else {
+		uint64_t Be = uni_offset >> 2;
+		if (Be >= 7 && Be + 9 <= ix->ref_bin_padded) {
+			uint64_t x = __builtin_bswap64(dsb_ld8u(ix->ref_bin + Be - 7)) >> (6 - 2 * (uint32_t)(uni_offset & 3));
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+			for (int k = 0; k < 8; k++) {
+				lo |= ((x >> (2 * k)) & 3) << (8 * k);
+				hi |= ((x >> (16 + 2 * k)) & 3) << (8 * k);
+			}
+			*lo_ = lo;
+			*hi_ = hi;
+			return;
+		}
 	}
+	uint64_t offset = uni_offset >> 2;
+	uint8_t odd = uni_offset & 0x3;
+	for (uint32_t k = 0; k < length && k < 16; k++) {
+		uint64_t b = (dsb_ref_byte(ix, offset) >> (6 - 2 * odd)) & 0x3;
+		if (k < 8) lo |= b << (8 * k);
+		else hi |= b << (8 * (k - 8));
+		if (isForward) { if (odd == 3) { odd = 0; offset++; } else odd++; }
+		else { if (odd == 0) { odd = 3; offset--; } else odd--; }
+	}
+	*lo_ = lo;
+	*hi_ = hi;
+}
+
+/*
+ * lv_extd on register windows: the terminators go into the register copies (the caller's
+ * windows are left as they are, as the reference restores them), and the in-line match
+ * `for (; ref[mn + j] == query[mn]; mn++)` compares 8 bytes per step (first differing byte of
+ * the XOR).  It always stops at query's '$' (ref holds no '$'), within the window.
+ * Same result as dsb_lv_extd for every input of that shape (tests/test_lv_words.py).
+ */
+DSB_HD int32_t dsb_lv_extd_r(dsb_w32 R, int32_t ref_length, dsb_w32 Q, int32_t query_length)
+{
 	if (ref_length < query_length) {
 		int32_t t = ref_length; ref_length = query_length; query_length = t;
-		for (int k = 0; k < 4; k++) { uint64_t x = R[k]; R[k] = Q[k]; Q[k] = x; }
+		dsb_w32 x = R; R = Q; Q = x;
 	}
-	dsb_set_byte(R, ref_length, '#');
-	dsb_set_byte(Q, query_length, '$');
+	dsb_w32_set_byte(R, ref_length, '#');
+	dsb_w32_set_byte(Q, query_length, '$');
 	int32_t mnd[2 * DSB_LV_ERROR + 5], edd[2 * DSB_LV_ERROR + 5];
 	int32_t *mn = mnd + DSB_LV_ERROR + 1, *ed = edd + DSB_LV_ERROR + 1;
 	int32_t prev_mn, cur_mn, next_mn, prev_ed, cur_ed, next_ed;
@@ -504,7 +584,7 @@ DSB_HD int32_t dsb_lv_extd_w(const uint8_t *ref_, int32_t ref_length, const uint
 			int mn_j = DSB_MIN(mn[j], query_length);
 			mn_j = DSB_MIN(mn_j, ref_length - j);
 			for (;;) { /* for (; ref[mn_j + j] == query[mn_j]; mn_j++) */
-				uint64_t x = dsb_win8(R, mn_j + j) ^ dsb_win8(Q, mn_j);
+				uint64_t x = dsb_w32_8(R, mn_j + j) ^ dsb_w32_8(Q, mn_j);
 				if (x) {
 					mn_j += __builtin_ctzll(x) >> 3;
 					break;
@@ -512,7 +592,7 @@ DSB_HD int32_t dsb_lv_extd_w(const uint8_t *ref_, int32_t ref_length, const uint
 				mn_j += 8;
 			}
 			mn[j] = mn_j;
-			if (dsb_byte_at(Q, mn_j) == '$' || dsb_byte_at(R, mn_j + j) == '#') {
+			if (dsb_w32_byte(Q, mn_j) == '$' || dsb_w32_byte(R, mn_j + j) == '#') {
 				best_score = DSB_MIN(ed[j] - 1, best_score);
 				if (j <= i + 1)
 					return best_score;
@@ -522,6 +602,11 @@ DSB_HD int32_t dsb_lv_extd_w(const uint8_t *ref_, int32_t ref_length, const uint
 		}
 	}
 	return best_score;
+}
+/* the same on 32-byte buffers in memory (ref_ / query_ point 8 bytes in) */
+DSB_HD int32_t dsb_lv_extd_w(const uint8_t *ref_, int32_t ref_length, const uint8_t *query_, int32_t query_length)
+{
+	return dsb_lv_extd_r(dsb_w32_load(ref_ - 8), ref_length, dsb_w32_load(query_ - 8), query_length);
 }
 
 /* ------------------------------------------------------------------ glibc msort */
