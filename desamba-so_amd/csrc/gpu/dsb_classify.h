@@ -471,7 +471,7 @@ DSB_HD int dsb_mem_search(dsb_read_ws *w, const uint8_t *string, uint64_t pre_v,
 {
 	const dsb_dindex_t *ix = w->ix;
 	int n_rst = 0;
-	uint64_t sp = ix->hash_index[pre_v], ep = ix->hash_index[pre_v + 1], new_sp, new_ep;
+	uint64_t sp = dsb_gld(ix->hash_index + pre_v), ep = dsb_gld(ix->hash_index + pre_v + 1), new_sp, new_ep;
 	if (w->stats) w->stats[DSB_ST_MEMSEARCH]++;
 	string -= DSB_L_PRE_IDX;
 	int match_len = DSB_L_PRE_IDX;
@@ -521,15 +521,15 @@ DSB_HD int dsb_mem_search(dsb_read_ws *w, const uint8_t *string, uint64_t pre_v,
 DSB_HD uint32_t dsb_get_uni(const dsb_dindex_t *ix, uint64_t bwt_pos, int search_l, uint64_t *global_offset,
 			     uint32_t *uni_offset_)
 {
-	dsb_sa_t s = ix->sa[bwt_pos >> 3];
+	dsb_sa_t s = dsb_gld(ix->sa + (bwt_pos >> 3));
 	uint32_t u = s.unitig_ID;
 	uint32_t uni_offset = s.offset + search_l + 1;
 	if (search_l > 0)
-		for (; uni_offset >= ix->uni[u].length && u < ix->n_uni;) { /* sentinel stops the walk */
-			uni_offset -= (ix->uni[u].length + 1);
+		for (; uni_offset >= dsb_gld(ix->uni + u).length && u < ix->n_uni;) { /* sentinel stops the walk */
+			uni_offset -= (dsb_gld(ix->uni + u).length + 1);
 			u++;
 		}
-	uint64_t rp = ix->r_p[ix->uni[u].ref_list];
+	uint64_t rp = dsb_gld(ix->r_p + dsb_gld(ix->uni + u).ref_list);
 	*global_offset = DSB_RP_OFF(rp) + uni_offset;
 	*uni_offset_ = uni_offset;
 	return u;
@@ -626,7 +626,7 @@ typedef struct { uint8_t *bin_read; uint32_t read_L; uint16_t seed_ID; uint32_t 
  * (unpinned); the device table is padded and the index clamped. */
 DSB_HD int dsb_qmem(const dsb_dindex_t *ix, uint32_t l)
 {
-	return ix->Q_MEM[l < DSB_Q_MEM_PAD ? l : DSB_Q_MEM_PAD - 1];
+	return dsb_gld(ix->Q_MEM + (l < DSB_Q_MEM_PAD ? l : DSB_Q_MEM_PAD - 1));
 }
 
 DSB_HD dsb_anchor_t *dsb_push_anchor(dsb_read_ws *w)
@@ -701,13 +701,13 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 				l_pre = s_l;
 		}
 		if (uni >= 0) {
-			if (ix->uni[uni].length < DSB_MIN_UNI_L)
+			if (dsb_gld(ix->uni + uni).length < DSB_MIN_UNI_L)
 				break;
 			l_pre = DSB_MIN(l_pre, u_off);
 			dsb_get_ref_r(w, TP, t_off - 1, l_pre, 0);
 		}
 		d_pre = dsb_lv_extd_r(TP, l_pre, QP, l_pre);
-		s = dsb_qmem(ix, l_m) + Q_LV[d_pre * DSB_LV_DIM + l_pre];
+		s = dsb_qmem(ix, l_m) + dsb_gld(Q_LV + (d_pre * DSB_LV_DIM + l_pre));
 		if (s < DSB_MIN_S_1 && l_pre == DSB_LV_L && uni < 0) {
 			s = 0;
 			break;
@@ -719,13 +719,13 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 				s_l++;
 			}
 			uni = (int32_t)dsb_get_uni_w(w, b_p, s_l, &t_off, &u_off);
-			if (ix->uni[uni].length < DSB_MIN_UNI_L) {
+			if (dsb_gld(ix->uni + uni).length < DSB_MIN_UNI_L) {
 				s = 0;
 				break;
 			}
 		}
 		int32_t q_off_r = q_off + l_m + 1;
-		uint32_t l_max_suf = DSB_MIN(ix->uni[uni].length - u_off - l_m, s_i->read_L - q_off_r);
+		uint32_t l_max_suf = DSB_MIN(dsb_gld(ix->uni + uni).length - u_off - l_m, s_i->read_L - q_off_r);
 		if (l_max_suf != 0) {
 			l_suf = DSB_MIN(l_max_suf, (uint32_t)DSB_LV_L);
 			q_suf = q_b + q_off_r;
@@ -737,7 +737,7 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 					mtc = dsb_w32_mismatch(TS, ql, qh, l_suf);
 					if (mtc > 0) {
 						l_m += mtc;
-						s = dsb_qmem(ix, l_m) + Q_LV[d_pre * DSB_LV_DIM + l_pre];
+						s = dsb_qmem(ix, l_m) + dsb_gld(Q_LV + (d_pre * DSB_LV_DIM + l_pre));
 						l_max_suf -= mtc;
 						l_suf = DSB_MIN(l_max_suf, (uint32_t)DSB_LV_L);
 						q_suf += mtc;
@@ -749,7 +749,7 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 			}
 			/* lv_extd terminates a copy of the read's bytes (q_suf - 8 .. q_suf + 24) */
 			d_suf = dsb_lv_extd_r(TS, l_suf, dsb_w32_load(q_suf - 8), l_suf);
-			s += Q_LV[d_suf * DSB_LV_DIM + l_suf];
+			s += dsb_gld(Q_LV + (d_suf * DSB_LV_DIM + l_suf));
 		} else
 			l_suf = d_suf = 0;
 		if (s <= DSB_MIN_S_2 && l_suf == DSB_LV_L) {
@@ -768,7 +768,7 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 		cx->am_mtch = (uint16_t)l_m;
 		cx->am_score = (int16_t)s;
 		cx->am_ll = (uint8_t)l_pre; cx->am_le = (uint8_t)d_pre; cx->am_rl = (uint8_t)l_suf; cx->am_re = (uint8_t)d_suf;
-		uint64_t rp_s = ix->uni[uni].ref_list, rp_e = ix->uni[uni + 1].ref_list;
+		uint64_t rp_s = dsb_gld(ix->uni + uni).ref_list, rp_e = dsb_gld(ix->uni + uni + 1).ref_list;
 		cx->ref_l = (uint8_t)(l_pre < DSB_LV_L || d_pre == 0);
 		cx->ref_r = (uint8_t)(l_suf < DSB_LV_L || d_suf == 0);
 		if (rp_e - rp_s > 50 && !(rp_e - rp_s < 1000)) {
@@ -785,7 +785,7 @@ DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, c
 {
 	const dsb_dindex_t *ix = w->ix;
 	const int *Q_LV = ix->Q_LV;
-	uint64_t rp = ix->r_p[cx->rp_s + item];
+	uint64_t rp = dsb_gld(ix->r_p + cx->rp_s + item);
 	if (w->stats) w->stats[DSB_ST_REFPOS]++;
 	uint16_t am_mtch = cx->am_mtch;
 	int16_t am_score = cx->am_score;
@@ -808,7 +808,7 @@ DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, c
 			am_re = (uint8_t)ed_r;
 			am_mtch = (uint16_t)(am_mtch + l_m_ext_r);
 		}
-		am_score = (int16_t)(dsb_qmem(ix, am_mtch) + Q_LV[am_le * DSB_LV_DIM + am_ll] + Q_LV[am_re * DSB_LV_DIM + am_rl]);
+		am_score = (int16_t)(dsb_qmem(ix, am_mtch) + dsb_gld(Q_LV + (am_le * DSB_LV_DIM + am_ll)) + dsb_gld(Q_LV + (am_re * DSB_LV_DIM + am_rl)));
 		if (am_score < DSB_MIN_S_2)
 			return 0;
 	}
@@ -816,7 +816,7 @@ DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, c
 	a->index_in_read = cx->q_off + 1 - l_m_ext_l;
 	a->global_offset = DSB_RP_OFF(rp) + cx->u_off - l_m_ext_l;
 	a->ref_ID = DSB_RP_REF(rp);
-	a->ref_offset = (uint32_t)(a->global_offset - ix->ref_seq_offset[a->ref_ID]);
+	a->ref_offset = (uint32_t)(a->global_offset - dsb_gld(ix->ref_seq_offset + a->ref_ID));
 	a->mtch_len = am_mtch;
 	a->score = am_score;
 	a->left_len = am_ll; a->left_ED = am_le; a->rigt_len = am_rl; a->rigt_ED = am_re;
@@ -1413,8 +1413,8 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 				uint64_t pre_v = w->pre[(s_d->strand ? w->L : 0) + (uint32_t)kmer_index];
 				string_index = kmer_index + l_ek - 1;
 				if (w->stats) w->stats[DSB_ST_MEMSEARCH]++;
-				sp = ix->hash_index[pre_v];
-				ep = ix->hash_index[pre_v + 1];
+				sp = dsb_gld(ix->hash_index + pre_v);
+				ep = dsb_gld(ix->hash_index + pre_v + 1);
 				str = bin_read + string_index - DSB_L_PRE_IDX;
 				match_len = DSB_L_PRE_IDX;
 				l_max = string_index;
@@ -1921,7 +1921,7 @@ DSB_HD void dsb_get_ref_win(dsb_read_ws *w, uint8_t *ref_str, uint64_t uni_offse
 				uint64_t B = pos0 >> 2;
 				uint64_t out = 0;
 				if (B + 16 <= w->ix->ref_bin_padded) {
-					uint64_t v = __builtin_bswap64(dsb_ld8u(w->ix->ref_bin + B));
+					uint64_t v = __builtin_bswap64(dsb_gld8u(w->ix->ref_bin + B));
 					uint32_t sh = (uint32_t)(pos0 & 3);
 					for (int j = 0; j < 8; j++)
 						out |= ((v >> (62 - 2 * (sh + j))) & 3) << (8 * j);
@@ -2454,7 +2454,7 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 	int score = 10000;
 	if (c_a_i < 0)
 		return score - 10000;
-	uint64_t t_offset = ix->ref_seq_offset[w->anc[c_a_i].ref_ID];
+	uint64_t t_offset = dsb_gld(ix->ref_seq_offset + w->anc[c_a_i].ref_ID);
 	while (c_a_i >= 0) {
 		dsb_anchor_t *c_a = w->anc + c_a_i;
 		int32_t pre_i = c_a->pre;
@@ -2626,8 +2626,8 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 	p->t_pos = c_h->t_ed;
 	p->len = 1 - DSB_S_A_KMER_L;
 	uint32_t current_sms = 1;
-	uint64_t t_offset_global = ix->ref_seq_offset[c_h->ref_ID];
-	uint64_t t_length = ix->ref_seq_l[c_h->ref_ID];
+	uint64_t t_offset_global = dsb_gld(ix->ref_seq_offset + c_h->ref_ID);
+	uint64_t t_length = dsb_gld(ix->ref_seq_l + c_h->ref_ID);
 	uint32_t c_t_offset = c_h->t_ed - 3;
 	int last_search = 0;
 	while (1) {
@@ -2774,7 +2774,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 	p->q_pos = c_h->q_st;
 	p->t_pos = c_h->t_st;
 	uint32_t current_sms = 1;
-	uint64_t t_offset_global = ix->ref_seq_offset[c_h->ref_ID];
+	uint64_t t_offset_global = dsb_gld(ix->ref_seq_offset + c_h->ref_ID);
 	uint32_t c_t_offset = c_h->t_st + 3;
 	int last_search = 0;
 	while (1) {

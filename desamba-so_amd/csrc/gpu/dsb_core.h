@@ -42,16 +42,39 @@
 #define DSB_HEAP_PERTURB 0x5A
 
 /* 8 bytes at p (any alignment) from the two aligned words covering them; may read up to 15
- * bytes past p, which stay inside the read's workspace arena (guards, or the next region). */
+ * bytes past p, which stay inside the read's workspace arena (guards, or the next region).
+ * The aligned address is formed by pointer arithmetic on p (not from an integer), so that the
+ * compiler keeps p's address space: global or LDS loads instead of generic (flat) ones. */
 DSB_HD uint64_t dsb_ld8u(const uint8_t *p)
 {
-	uintptr_t a = (uintptr_t)p;
-	const uint64_t *b = (const uint64_t *)(a & ~(uintptr_t)7);
-	uint32_t sh = (uint32_t)(a & 7) * 8;
+	uint32_t o = (uint32_t)((uintptr_t)p & 7);
+	const uint64_t *b = (const uint64_t *)(p - o);
+	uint32_t sh = o * 8;
 	uint64_t lo = b[0];
 	if (!sh)
 		return lo;
 	return (lo >> sh) | (b[1] << (64 - sh));
+}
+
+/* Loads from the index tables (device memory, dsb_dindex_t).  Their pointers are read from
+ * memory, so the compiler cannot infer their address space and would emit generic (flat) loads,
+ * which also count against the LDS / scalar wait counter; the explicit global address space
+ * gives global_load. */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DSB_AS_GLOBAL __attribute__((address_space(1)))
+#else
+#define DSB_AS_GLOBAL
+#endif
+template <typename T> DSB_HD T dsb_gld(const T *p) { return *(const DSB_AS_GLOBAL T *)p; }
+/* dsb_ld8u on an index table */
+DSB_HD uint64_t dsb_gld8u(const uint8_t *p)
+{
+	uint32_t o = (uint32_t)((uintptr_t)p & 7);
+	const uint64_t *b = (const uint64_t *)(p - o);
+	uint64_t lo = dsb_gld(b);
+	if (!o)
+		return lo;
+	return (lo >> (o * 8)) | (dsb_gld(b + 1) << (64 - o * 8));
 }
 
 /* ------------------------------------------------------------------ hashing */
@@ -88,10 +111,10 @@ DSB_HD int dsb_exist_kmer(const dsb_dindex_t *ix, uint64_t kmer)
 	if (kmer == 0)
 		return 0;
 	uint64_t h1 = dsb_hash64_1(kmer) & ix->ek_mask;
-	if (((ix->ek0[h1 >> 3] >> (7 - (h1 & 0x7))) & 0x1) == 0)
+	if (((dsb_gld(ix->ek0 + (h1 >> 3)) >> (7 - (h1 & 0x7))) & 0x1) == 0)
 		return 0;
 	uint64_t h2 = dsb_hash64_2(kmer) & ix->ek_mask;
-	return (ix->ek1[h2 >> 3] >> (7 - (h2 & 0x7))) & 0x1;
+	return (dsb_gld(ix->ek1 + (h2 >> 3)) >> (7 - (h2 & 0x7))) & 0x1;
 }
 
 /* CLY_Bit (src/cly.c:16-34): A/a->0 C/c->1 G/g->2 T/t->3, every other byte -> 1 ('C').
@@ -181,7 +204,7 @@ DSB_HD uint64_t dsb_occ(const dsb_dindex_t *ix, uint64_t r, uint8_t *c)
 #pragma unroll
 #endif
 	for (int k = 0; k < DSB_OCC_LINE_U64; k++)
-		v[k] = ln[k];
+		v[k] = dsb_gld(ln + k);
 	int within = (int)(r & 0xff);
 	if (*c == 0xff) {
 		int wi = within >> 5, si = within >> 6;
@@ -254,7 +277,7 @@ DSB_HD uint64_t dsb_lf(const dsb_dindex_t *ix, uint64_t r, uint8_t *c)
 /* ------------------------------------------------------------------ reference text */
 DSB_HD uint8_t dsb_ref_byte(const dsb_dindex_t *ix, uint64_t off)
 {
-	return off < ix->ref_bin_padded ? ix->ref_bin[off] : 0;
+	return off < ix->ref_bin_padded ? dsb_gld(ix->ref_bin + off) : 0;
 }
 
 /* get_ref, src/cly.c:434-461: 2-bit MSB-first unpack, forward or backward from uni_offset */
@@ -265,7 +288,7 @@ DSB_HD void dsb_get_ref(const dsb_dindex_t *ix, uint8_t *ref_str, uint64_t uni_o
 		if (isForward) {
 			uint64_t B = uni_offset >> 2;
 			if (B + 16 <= ix->ref_bin_padded) {
-				uint64_t v = __builtin_bswap64(dsb_ld8u(ix->ref_bin + B));
+				uint64_t v = __builtin_bswap64(dsb_gld8u(ix->ref_bin + B));
 				uint32_t m0 = (uint32_t)(uni_offset & 3);
 				for (uint32_t k = 0; k < length; k++)
 					ref_str[k] = (uint8_t)((v >> (62 - 2 * (m0 + k))) & 3);
@@ -274,7 +297,7 @@ DSB_HD void dsb_get_ref(const dsb_dindex_t *ix, uint8_t *ref_str, uint64_t uni_o
 		} else {
 			uint64_t Be = uni_offset >> 2;
 			if (Be >= 7 && Be + 9 <= ix->ref_bin_padded) {
-				uint64_t v = __builtin_bswap64(dsb_ld8u(ix->ref_bin + Be - 7));
+				uint64_t v = __builtin_bswap64(dsb_gld8u(ix->ref_bin + Be - 7));
 				uint32_t m0 = (uint32_t)(uni_offset & 3) + 28;
 				for (uint32_t k = 0; k < length; k++)
 					ref_str[k] = (uint8_t)((v >> (62 - 2 * (m0 - k))) & 3);
@@ -471,7 +494,7 @@ DSB_HD void dsb_get_ref16(const dsb_dindex_t *ix, uint64_t uni_offset, uint32_t 
 	if (isForward) {
 		uint64_t B = uni_offset >> 2;
 		if (B + 16 <= ix->ref_bin_padded) {
-			uint64_t y = __builtin_bswap64(dsb_ld8u(ix->ref_bin + B)) << (2 * (uint32_t)(uni_offset & 3));
+			uint64_t y = __builtin_bswap64(dsb_gld8u(ix->ref_bin + B)) << (2 * (uint32_t)(uni_offset & 3));
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
@@ -486,7 +509,7 @@ DSB_HD void dsb_get_ref16(const dsb_dindex_t *ix, uint64_t uni_offset, uint32_t 
 	} else {
 		uint64_t Be = uni_offset >> 2;
 		if (Be >= 7 && Be + 9 <= ix->ref_bin_padded) {
-			uint64_t x = __builtin_bswap64(dsb_ld8u(ix->ref_bin + Be - 7)) >> (6 - 2 * (uint32_t)(uni_offset & 3));
+			uint64_t x = __builtin_bswap64(dsb_gld8u(ix->ref_bin + Be - 7)) >> (6 - 2 * (uint32_t)(uni_offset & 3));
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif

@@ -28,9 +28,14 @@
 			   ((PH) == DSB_PH_FAST0 || (PH) == DSB_PH_FAST1 || (PH) == DSB_PH_SLOW0 || (PH) == DSB_PH_SLOW1) \
 			   ? DSB_MINW_FAST : DSB_MINW_RESOLVE)
 #define DSB_WIN_LDS_BYTES ((DSB_WIN_BYTES + 15) & ~15)
-/* scoring-phase LDS per wave: the reference windows (+ 64 B slack for the 8-byte word reads past
- * their end), and the sparse-DP prefix when DSB_SMS_IN_LDS */
-#define DSB_DELA_LDS (DSB_WIN_LDS_BYTES + 64 + (DSB_SMS_IN_LDS ? DSB_SMS_LDS * sizeof(dsb_spd_t) : 0))
+/* The scoring phase's reference windows (sdp_middle ref[2000], sdp_right/left ref[1000]) live in
+ * LDS, in the same 4 KB the read-hash build uses for its key-group slots before the first window
+ * is loaded (every window byte a scan reads is written in the same call: DESIGN.md §5), so the
+ * kernel keeps its 8 waves per SIMD.  DSB_WIN_IN_LDS=0 keeps them in the workspace (HBM). */
+#ifndef DSB_WIN_IN_LDS
+#define DSB_WIN_IN_LDS 1
+#endif
+#define DSB_DELA_LDS_BYTES (DSB_WIN_LDS_BYTES + 64 > DSB_HB_LDS ? DSB_WIN_LDS_BYTES + 64 : DSB_HB_LDS)
 static_assert(sizeof(dsb_rstate_t) <= DSB_STATE_BYTES, "per-read phase state must fit its workspace slot");
 
 /* One phase of classify part A (dsb_phase), one lane per read; the read's control state
@@ -179,11 +184,6 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
 		w.stats = st;
 	}
-	if (PH == DSB_PH_DELA && (dbg & 512)) { /* scoring: reference windows and the sparse-DP prefix in LDS */
-		extern __shared__ uint8_t dsb_lds[];
-		w.win = dsb_lds;
-		w.sms_lds = DSB_SMS_IN_LDS ? (dsb_spd_t *)(dsb_lds + DSB_WIN_LDS_BYTES + 64) : 0;
-	}
 	int active = dsb_phase_active(&w, &f, ph);
 	if (active) {
 		if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
@@ -205,8 +205,10 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 			w.lds_id = sort_id;
 			dsb_phase<true>(&w, &f, ph);
 		} else if (ph == DSB_PH_DELA) {
-			__shared__ uint8_t hb_lds[DSB_HB_LDS];
-			w.lds_hb = hb_lds;
+			__shared__ uint64_t dela_lds[DSB_DELA_LDS_BYTES / 8];
+			w.lds_hb = (uint8_t *)dela_lds;
+			if (DSB_WIN_IN_LDS)
+				w.win = (uint8_t *)dela_lds;
 			dsb_phase<true>(&w, &f, ph);
 		} else
 			dsb_phase<true>(&w, &f, ph);

@@ -423,14 +423,11 @@ static uint64_t seed_words(const std::vector<uint32_t> &len, uint64_t cb, const 
 	return tw;
 }
 
-/* diagnostics / experiments: DSB_WAVE_DBG bits (dsb_classify.h), DSB_LDS=1 -> bit 512 */
+/* diagnostics / experiments: DSB_WAVE_DBG bits (dsb_classify.h) */
 static uint32_t wave_dbg(void)
 {
 	const char *e = getenv("DSB_WAVE_DBG");
 	uint32_t d = e ? (uint32_t)strtoul(e, NULL, 0) : 0;
-	const char *l = getenv("DSB_LDS");
-	if (l && atoi(l))
-		d |= 512;
 	return d;
 }
 
@@ -467,7 +464,7 @@ static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl,
 	}
 	uint32_t tag = g->tag;
 	if (wave)
-		hipLaunchKernelGGL(fn, dim3(m), dim3(64), (ph == DSB_PH_DELA && (dbg & 512)) ? DSB_DELA_LDS : 0, s, g->d, cl,
+		hipLaunchKernelGGL(fn, dim3(m), dim3(64), 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
 				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), dbg, tag);
 	else

@@ -92,13 +92,14 @@ int main(int argc, char **argv)
 					}
 				}
 			}
-			static uint8_t lds_win[DSB_WIN_BYTES];
+			static uint8_t lds_win[DSB_WIN_BYTES + DSB_HB_LDS + 64];
 			static dsb_spd_t lds_sms[DSB_SMS_LDS];
 			if (getenv("EMU_LDS")) { /* the scoring kernel's LDS layout (separate window / sms prefix) */
 				int fill = (int)strtol(getenv("EMU_LDS"), 0, 0); /* garbage left by other workgroups */
 				memset(lds_win, fill, sizeof(lds_win));
 				memset(lds_sms, fill, sizeof(lds_sms));
-				w.win = lds_win;
+				w.win = lds_win; /* the scoring kernel's windows share their LDS with the hash-build slots */
+				w.lds_hb = lds_win;
 				w.sms_lds = lds_sms;
 			}
 			if (getenv("EMU_WAVE")) { /* the wave-cooperative code paths, as a one-lane wave */
