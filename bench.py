@@ -211,7 +211,7 @@ def main():
     def step():
         tm = batch.run(max_read_l=0)
         tid, _ = batch.taxa(0)
-        counts.copy_(shard.reduce_counts(shard.taxon_counts(tid, None, n_tax), cdev))
+        counts.copy_(shard.reduce_counts(shard.taxon_counts(tid, None, n_tax, cdev), cdev))
         return tm
 
     for _ in range(a.warmup):

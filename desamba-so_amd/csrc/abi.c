@@ -38,6 +38,13 @@ static void fatal(const char *func, const char *msg)
 	exit(1);
 }
 
+/* taxid of "tid|<taxid>|..." reference names (getOneSAM, src/cly_mt.c:778-786) */
+static uint32_t name_taxid(const char *name)
+{
+	const char *p = strchr(name, '|');
+	return p ? (uint32_t)strtoul(p + 1, NULL, 10) : 0;
+}
+
 void load_index(void **idx, const char *dirPath)
 {
 	char err[1024];
@@ -49,6 +56,9 @@ void load_index(void **idx, const char *dirPath)
 	ix->filter_min_score_LV3 = 64 + 10;
 	dsb_mapq_tables(ix, 0.15, ix->ref_bin_n * 4);
 	if (dsb_taxonomy_load(ix, dirPath, err, sizeof(err))) fatal("load_index", err);
+	ix->ref_tid = malloc(sizeof(uint32_t) * (ix->n_ref + 1));
+	for (uint64_t r = 0; r < ix->n_ref; r++)
+		ix->ref_tid[r] = name_taxid(ix->ref_name[r]);
 	if (dsb_gpu_init(ix, -1, err, sizeof(err))) fatal("load_index", err);
 	if (!getenv("DSB_KEEP_HOST_TABLES"))
 		dsb_index_free_host_tables(ix);
@@ -253,13 +263,6 @@ int dsb_batch_format_range(void *idx, dsb_batch *b, int format, uint64_t lo, uin
 	return 0;
 }
 
-/* taxid of "tid|<taxid>|..." reference names (getOneSAM, src/cly_mt.c:778-786) */
-static uint32_t name_taxid(const char *name)
-{
-	const char *p = strchr(name, '|');
-	return p ? (uint32_t)strtoul(p + 1, NULL, 10) : 0;
-}
-
 int dsb_batch_taxa(void *idx, dsb_batch *b, int flag, uint32_t *tid_out, uint64_t *weight_out)
 {
 	dsb_index *ix = idx;
@@ -269,17 +272,18 @@ int dsb_batch_taxa(void *idx, dsb_batch *b, int flag, uint32_t *tid_out, uint64_
 	uint32_t *rec_score = malloc(sizeof(uint32_t) * (DSB_MAX_HITS + 1));
 	for (uint64_t i = 0; i < b->reads.n; i++) {
 		const dsb_rec_t *rec = b->reads.rec + i;
+		/* the SAM text meta_analysis parses prints SEQ with %s: its length is strlen */
 		weight_out[i] = (flag & 1) ? (uint64_t)strlen(b->reads.arena + rec->seq_off) : 1;
 		uint32_t nh = ro[i].n_hit;
 		if (nh == 0) { tid_out[i] = 0; continue; }
 		const dsb_hit_out_t *h = hits + ro[i].hit_off;
 		/* SAM record order of output_one_result_sam: primary, supplementaries, secondaries */
 		uint32_t nr = 0;
-		rec_tid[nr] = name_taxid(ix->ref_name[h[0].ref_ID]); rec_score[nr++] = h[0].sum_score;
+		rec_tid[nr] = ix->ref_tid[h[0].ref_ID]; rec_score[nr++] = h[0].sum_score;
 		for (int loop = 0; loop <= 1; loop++)
 			for (uint32_t k = 1; k < nh; k++)
 				if ((loop == 0 && h[k].pri_index == 0) || (loop == 1 && h[k].pri_index > 0 && h[k].pri_index <= 5)) {
-					rec_tid[nr] = name_taxid(ix->ref_name[h[k].ref_ID]);
+					rec_tid[nr] = ix->ref_tid[h[k].ref_ID];
 					rec_score[nr++] = h[k].sum_score;
 				}
 		/* ana_get_tid: an equal-score later record of a descendant taxon wins */
@@ -341,7 +345,7 @@ void dsb_unload_index(void *idx)
 	if (!ix) return;
 	dsb_gpu_free(ix);
 	dsb_index_free_host_tables(ix);
-	free(ix->Q_MEM); free(ix->ref_name); free(ix->ref_seq_l); free(ix->ref_seq_offset); free(ix->tax);
+	free(ix->Q_MEM); free(ix->ref_name); free(ix->ref_tid); free(ix->ref_seq_l); free(ix->ref_seq_offset); free(ix->tax);
 	struct dsb_thread_state *s = ix->states;
 	while (s) { struct dsb_thread_state *n = s->next; free(s); s = n; }
 	pthread_mutex_destroy(&ix->state_mutex);

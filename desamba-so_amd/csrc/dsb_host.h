@@ -38,6 +38,7 @@ typedef struct dsb_index {
 	uint8_t *ref_bin; uint64_t ref_bin_n, ref_bin_padded;
 	uint64_t n_ref;
 	char (*ref_name)[128];
+	uint32_t *ref_tid;        /* taxid of each reference name ("tid|<taxid>|...", cly_mt.c:778-786) */
 	uint64_t *ref_seq_l, *ref_seq_offset;
 	uint64_t *r_p; uint64_t n_rp;
 	int *Q_MEM;               /* DSB_Q_MEM_PAD */

@@ -409,6 +409,9 @@ DSB_HD void dsb_set_reset(dsb_hset_t *s)
 }
 DSB_HD int dsb_set_insert(uint64_t node, dsb_hset_t *s)
 {
+#ifdef DSB_EXP_NO_HSET
+	return 1; /* timing experiment only: no duplicate detection */
+#endif
 	if (s->l == s->m) {
 		s->l = 0;
 		s->gen++;
@@ -1911,7 +1914,7 @@ DSB_HD void dsb_get_ref_win(dsb_read_ws *w, uint8_t *ref_str, uint64_t uni_offse
 		uint64_t b0 = uni_offset >> 2;
 		uint32_t odd = (uint32_t)(uni_offset & 3);
 #ifndef DSB_WIN_WORDS
-#define DSB_WIN_WORDS 0 /* 8-base stores raise the scoring kernel's spills 40 -> 105: off */
+#define DSB_WIN_WORDS 1 /* 8 bases per lane and load (with the windows in LDS: 83 -> 78 ms) */
 #endif
 		if (DSB_WIN_WORDS && ((uintptr_t)ref_str & 7) == 0) {
 			/* 8 bases per lane: one 8-byte window of the packed reference, one 8-byte store

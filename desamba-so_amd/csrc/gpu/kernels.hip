@@ -482,7 +482,25 @@ struct dsb_gpu_batch {
 	std::vector<dsb_read_out_t> ro;
 	std::vector<dsb_hit_out_t> hits;
 	std::vector<int32_t> carry; /* max_read_l each read's part B used (src/cly.c:2953) */
+	/* per-chunk processing order (longest first), cached: it depends on the lengths only */
+	std::vector<uint64_t> ord_cb, ord_ce;
+	std::vector<std::vector<uint32_t>> ord;
 };
+
+static const std::vector<uint32_t> &chunk_order(dsb_gpu_batch *b, uint64_t cb, uint64_t ce)
+{
+	for (size_t k = 0; k < b->ord.size(); k++)
+		if (b->ord_cb[k] == cb && b->ord_ce[k] == ce)
+			return b->ord[k];
+	std::vector<uint32_t> order(ce - cb);
+	for (uint32_t i = 0; i < ce - cb; i++) order[i] = i;
+	const std::vector<uint32_t> &len = b->len;
+	std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t c) { return len[cb + a] > len[cb + c]; });
+	b->ord_cb.push_back(cb);
+	b->ord_ce.push_back(ce);
+	b->ord.push_back(std::move(order));
+	return b->ord.back();
+}
 
 static int batch_upload(dsb_gpu_dev *g, const dsb_reads_t *reads, dsb_gpu_batch *b, dsb_gpu_timing &T, char *err,
 			size_t errn)
@@ -676,9 +694,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		const uint32_t *cl = b->d_len.as<uint32_t>() + cb;
 		const uint64_t *cso = b->d_seq_off.as<uint64_t>() + cb;
 		/* length-sorted order (longest first) for the one-lane-per-read kernels */
-		std::vector<uint32_t> order(cn);
-		for (uint32_t i = 0; i < cn; i++) order[i] = i;
-		std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return len[cb + a] > len[cb + b]; });
+		const std::vector<uint32_t> &order = chunk_order(b, cb, ce);
 		HIP_OK(hipMemcpyAsync(g->order.p, order.data(), 4ull * cn, hipMemcpyHostToDevice, s));
 		uint8_t *wsb = g->ws.as<uint8_t>();
 		hipEventRecord(g->ev_a, s);

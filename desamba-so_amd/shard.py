@@ -72,11 +72,21 @@ def carry_rerun_prefix(carry, p_earlier: int) -> int:
     return k
 
 
-def taxon_counts(tid, weight, n_tax: int):
-    """Per-taxon weights of one shard (meta_analysis node_count, src/cly_mt.c:1352-1362)."""
+def taxon_counts(tid, weight, n_tax: int, device=None):
+    """Per-taxon weights of one shard (meta_analysis node_count, src/cly_mt.c:1352-1362).
+    device=None: a numpy table; otherwise the table is counted there (torch.bincount; integer
+    weights, exact)."""
     import numpy as np
-    return np.bincount(np.asarray(tid, dtype=np.int64), weights=None if weight is None else
-                       np.asarray(weight, dtype=np.float64), minlength=n_tax).astype(np.int64)
+    if device is None:
+        return np.bincount(np.asarray(tid, dtype=np.int64), weights=None if weight is None else
+                           np.asarray(weight, dtype=np.float64), minlength=n_tax).astype(np.int64)
+    import torch
+    t = torch.from_numpy(np.asarray(tid, dtype=np.int64)).to(device, non_blocking=False)
+    if weight is None:
+        return torch.bincount(t, minlength=n_tax)
+    wt = torch.from_numpy(np.asarray(weight, dtype=np.int64)).to(device)
+    out = torch.zeros(n_tax, dtype=torch.int64, device=device)
+    return out.index_add_(0, t, wt)
 
 
 def reduce_counts(counts, device="cpu"):
