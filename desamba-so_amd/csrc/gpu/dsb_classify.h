@@ -952,6 +952,12 @@ DSB_HDN void dsb_fast_classify(dsb_read_ws *w, const dsb_sdir_t *s_d)
  * seed in order.  SLOW (slow_classify, src/cly.c:1545-1606): every seed the reference takes,
  * every 2nd k-mer, up to 8 rows per FM hit, the seed's stable top-8 hits mapped at its end.
  */
+/* DSB_SEED_PRE 1: k_seed stores every position's 13-mer prefix value (u32, 6.4 GB at C1) for
+ * the J step; 0: the J step recomputes it from the read (three word loads).  Measured on
+ * C1: k_seed -1.3 ms, fast seeding +1.6 ms: kept at 1 */
+#ifndef DSB_SEED_PRE
+#define DSB_SEED_PRE 1
+#endif
 #ifndef DSB_SM_MAP_BATCH
 #define DSB_SM_MAP_BATCH 64
 #endif
@@ -1413,7 +1419,8 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 			} else {
 				int kmer_index = (int)seed_off + j;
 				/* (kmer_at(...) & DSB_PRE_IDX_MASK), computed once per position by k_seed */
-				uint64_t pre_v = w->pre[(s_d->strand ? w->L : 0) + (uint32_t)kmer_index];
+				uint64_t pre_v = DSB_SEED_PRE ? w->pre[(s_d->strand ? w->L : 0) + (uint32_t)kmer_index]
+							      : (dsb_kmer_at(bin_read + kmer_index, l_ek, ix->single_base_max) & DSB_PRE_IDX_MASK);
 				string_index = kmer_index + l_ek - 1;
 				if (w->stats) w->stats[DSB_ST_MEMSEARCH]++;
 				sp = dsb_gld(ix->hash_index + pre_v);

@@ -96,11 +96,13 @@ __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ i
 	dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, DSB_SCALE_UNIT)); /* ex offsets do not depend on caps */
 	uint64_t *ex = (uint64_t *)(base + (strand ? lay.exR : lay.exF));
 	uint32_t *pre = (uint32_t *)(base + lay.pre) + (strand ? L : 0);
+	(void)pre;
 	uint32_t k = word * 64 + lane;
 	int e = 0;
 	if (k < lk) {
 		uint64_t km = dsb_kmer_at(bin + k, l_ek, ix->single_base_max);
-		pre[k] = (uint32_t)(km & DSB_PRE_IDX_MASK); /* the seeding's 13-mer prefix (fast / slow J step) */
+		if (DSB_SEED_PRE)
+			pre[k] = (uint32_t)(km & DSB_PRE_IDX_MASK); /* the seeding's 13-mer prefix (fast / slow J step) */
 		e = dsb_exist_kmer(ix, km);
 	}
 	uint64_t bits = __ballot(e);
