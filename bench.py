@@ -241,7 +241,12 @@ def main():
     roof = None
     stats = None
     if not a.no_stats:
-        ts = batch.run(max_read_l=0, stats=True)
+        ts = batch.run(max_read_l=0, stats=1)
+        tt = batch.run(max_read_l=0, stats=2)  # wave clocks: a run of its own (no counter traffic)
+        for ph, c in ts["stats_phase"].items():
+            for k in c:
+                if k.startswith("t_") and k not in ("t_dpm", "t_dps", "t_fill") or (ph == "delA" and k.startswith("t_")):
+                    c[k] = tt["stats_phase"][ph][k]
         per_phase = {}
         for ph, c in ts["stats_phase"].items():
             b = phase_bytes(c) + (batch.n_bases if ph in ("fast0", "slow0") else 0)

@@ -28,6 +28,7 @@ typedef struct dsb_index {
 	/* host copies (big tables are released after the device upload unless kept) */
 	uint8_t *bwt_occ; uint64_t byteLen;  /* the file's 168-B blocks (freed after the re-layout) */
 	uint64_t *occ; uint64_t n_occ_line; /* HBM layout, dsb_types.h */
+	uint64_t *occ_super; uint64_t n_occ_super;
 	uint64_t dollar_row[DSB_MAX_DOLLAR]; int n_dollar;
 	uint64_t rank[6];
 	uint64_t *hash_index;

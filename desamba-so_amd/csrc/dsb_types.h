@@ -31,19 +31,23 @@ typedef struct { uint32_t ref_list, length; } dsb_unitig_t;
 #define DSB_MIN_UNI_L 35
 #define DSB_MIN_READ_LEN 40
 #define DSB_MAX_DOLLAR 4     /* '$' symbols in the BWT the HBM occ layout supports (one in practice) */
-#define DSB_OCC_LINE_U64 16  /* u64 words per 256-symbol occ line */
+#define DSB_OCC_LINE_U64 8   /* u64 words per occ line (64 B) */
+#define DSB_OCC_LINE_SYM 128 /* BWT symbols per occ line */
+#define DSB_OCC_SUPER_SHIFT 17 /* lines per superblock: 2^17 (2^24 symbols; line counts are relative to it) */
 
 /*
  * Device-visible index: raw pointers into HBM (or host memory for the
  * kernel-logic CPU emulation used only by tests).
  */
 typedef struct {
-	/* occ/rank table re-laid out for HBM: one 128-B line per 256 BWT symbols,
-	 * u64 cnt[4] (occ of A,C,G,T at the line start) | u64 sym[8] (2-bit symbols, 32 per word,
-	 * '#'/'$' stored as 0) | u64 spc[4] (1 = '#' or '$', 64 per word).  Replaces the
-	 * reference's 168-B blocks (bwt.c:32-42) losslessly: '$' rows are listed below and the
+	/* occ/rank table re-laid out for HBM: one 64-B line per 128 BWT symbols,
+	 * u32 cnt[4] (occ of A,C,G,T at the line start, relative to its superblock) | u64 sym[4]
+	 * (2-bit symbols, 32 per word, '#'/'$' stored as 0) | u64 spc[2] (1 = '#' or '$', 64 per
+	 * word); occ_super: u64 cnt[4] at the start of every 2^DSB_OCC_SUPER_SHIFT lines.  Replaces
+	 * the reference's 168-B blocks (bwt.c:32-42) losslessly: '$' rows are listed below and the
 	 * '#' count is line start - A - C - G - T - '$' before it. */
 	const uint64_t *occ;
+	const uint64_t *occ_super;
 	uint64_t n_occ_line;
 	uint64_t dollar_row[DSB_MAX_DOLLAR];
 	int n_dollar;

@@ -121,6 +121,7 @@ typedef struct {
 	uint64_t *stats;
 	uint32_t dbg;           /* diagnostics: force sequential variants of the wave loops */
 	uint32_t launch_tag;    /* unique per kernel launch (host counter, never 0): seeding sp_set slot tags */
+	uint64_t *tmr;          /* timer kernels: wave clocks per DSB_ST_T_* slot (LDS, lane 0), or 0 */
 } dsb_read_ws;
 
 enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, DSB_ST_REFPOS,
@@ -139,8 +140,10 @@ enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, 
        DSB_ST_T_DPS,    /* sdp_right / sdp_left predecessor scans */
        DSB_ST_T_FILL,   /* stack-pattern fills of the windows */
        DSB_ST_N };
-#define DSB_T0() ((w->stats && dsb_lane() == 0) ? dsb_clock() : 0)
-#define DSB_T1(slot, t0) do { if (w->stats && dsb_lane() == 0) w->stats[slot] += dsb_clock() - (t0); } while (0)
+/* wave clocks of a code region (timer kernels only: lane 0 accumulates into LDS, so that the
+ * timing run pays no private-memory traffic for its counters) */
+#define DSB_T0() ((w->tmr && dsb_lane() == 0) ? dsb_clock() : 0)
+#define DSB_T1(slot, t0) do { if (w->tmr && dsb_lane() == 0) w->tmr[slot] += dsb_clock() - (t0); } while (0)
 
 DSB_HD uint64_t dsb_clock(void)
 {
@@ -876,10 +879,10 @@ DSB_HD int dsb_fast_seed(dsb_read_ws *w, const dsb_sdir_t *s_d, uint32_t ci, SET
 		uint64_t kmer = dsb_kmer_at(bin_read + kmer_index, l_ek, ix->single_base_max);
 		uint64_t prefixValue = kmer & DSB_PRE_IDX_MASK;
 		int string_index = kmer_index + l_ek - 1;
-		uint64_t t0 = w->stats ? dsb_clock() : 0;
+		uint64_t t0 = w->tmr ? dsb_clock() : 0;
 		int n_m = dsb_mem_search(w, bin_read + string_index, prefixValue, DSB_MEM_SEARCH_FAST,
 					 DSB_MIN_MEM_LEN_FAST - 1, string_index, sp_set, m_r);
-		if (w->stats) w->stats[DSB_ST_T_MEM] += dsb_clock() - t0;
+		if (w->tmr) w->tmr[DSB_ST_T_MEM] += dsb_clock() - t0;
 		if (n_m == 0) {
 			j -= 2;
 			continue;
@@ -888,9 +891,9 @@ DSB_HD int dsb_fast_seed(dsb_read_ws *w, const dsb_sdir_t *s_d, uint32_t ci, SET
 		int max_score = 0;
 		for (int k = 0; k < n_m; k++) {
 			m_r[k].read_offset = string_index - m_r[k].match_len;
-			uint64_t t1 = w->stats ? dsb_clock() : 0;
+			uint64_t t1 = w->tmr ? dsb_clock() : 0;
 			int c_score = dsb_map_seed(w, m_r + k, &s_i);
-			if (w->stats) w->stats[DSB_ST_T_MAP] += dsb_clock() - t1;
+			if (w->tmr) w->tmr[DSB_ST_T_MAP] += dsb_clock() - t1;
 			max_score = DSB_MAX(c_score, max_score);
 		}
 		if (w->overflow)

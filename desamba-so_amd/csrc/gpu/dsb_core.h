@@ -193,32 +193,34 @@ DSB_HD uint64_t dsb_low_mask(int n) /* low n (0..64) bits */
 /*
  * occ, src/bwt.c:43-65: number of c in BWT[0, r) — the line's checkpoint + the matching
  * symbols before r in the line.  c == 0xff: c := symbol at r, and '$' (5) returns DOLLOR_POS.
- * One 128-B line per 256 symbols (dsb_types.h): the whole line is fetched with independent
- * loads (one memory round trip), the symbol at r and the counts are computed from registers.
+ * One 64-B line per 128 symbols (dsb_types.h): the line (four 16-B loads) and its superblock's
+ * four counts (two 16-B loads, a table that stays in L2) are fetched together, one memory
+ * round trip; the symbol at r and the counts are computed from registers.
  */
 DSB_HD uint64_t dsb_occ(const dsb_dindex_t *ix, uint64_t r, uint8_t *c)
 {
-	const uint64_t *ln = (const uint64_t *)__builtin_assume_aligned(ix->occ + (r >> 8) * DSB_OCC_LINE_U64, 128);
-	uint64_t v[DSB_OCC_LINE_U64];
+	uint64_t line = r / DSB_OCC_LINE_SYM;
+	const uint64_t *ln = (const uint64_t *)__builtin_assume_aligned(ix->occ + line * DSB_OCC_LINE_U64, 64);
+	const uint64_t *sp = (const uint64_t *)__builtin_assume_aligned(ix->occ_super + (line >> DSB_OCC_SUPER_SHIFT) * 4, 32);
+	uint64_t v[DSB_OCC_LINE_U64], su[4];
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
 	for (int k = 0; k < DSB_OCC_LINE_U64; k++)
 		v[k] = dsb_gld(ln + k);
-	int within = (int)(r & 0xff);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+	for (int k = 0; k < 4; k++)
+		su[k] = dsb_gld(sp + k);
+	int within = (int)(r % DSB_OCC_LINE_SYM);
 	if (*c == 0xff) {
-		int wi = within >> 5, si = within >> 6;
-		uint64_t sw = v[4], pw = v[12];
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
-		for (int k = 1; k < 8; k++)
-			sw = (wi == k) ? v[4 + k] : sw;
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
-		for (int k = 1; k < 4; k++)
-			pw = (si == k) ? v[12 + k] : pw;
+		int wi = within >> 5;
+		uint64_t sw = v[2];
+		sw = (wi == 1) ? v[3] : sw;
+		sw = (wi == 2) ? v[4] : sw;
+		sw = (wi == 3) ? v[5] : sw;
+		uint64_t pw = (within >> 6) ? v[7] : v[6];
 		if ((pw >> (within & 63)) & 1) {
 			*c = 4;
 			for (int d = 0; d < ix->n_dollar; d++)
@@ -230,33 +232,30 @@ DSB_HD uint64_t dsb_occ(const dsb_dindex_t *ix, uint64_t r, uint8_t *c)
 			*c = (uint8_t)((sw >> (2 * (within & 31))) & 3);
 	}
 	uint32_t cc = *c;
-	uint64_t pat = 0x5555555555555555ull * (cc & 3);
-	uint64_t base = v[0];
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
-	for (int k = 1; k < 4; k++)
-		base = (cc == (uint32_t)k) ? v[k] : base;
-	uint32_t spc = 0;
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
-	for (int k = 0; k < 4; k++)
-		spc += (uint32_t)__builtin_popcountll(v[12 + k] & dsb_low_mask(within - 64 * k));
+	uint32_t spc = (uint32_t)__builtin_popcountll(v[6] & dsb_low_mask(within)) +
+		       (uint32_t)__builtin_popcountll(v[7] & dsb_low_mask(within - 64));
 	if (cc < 4) {
+		uint64_t pat = 0x5555555555555555ull * (cc & 3);
+		uint32_t rel = (uint32_t)(v[cc >> 1] >> (32 * (cc & 1)));
+		uint64_t sub = su[0];
+		sub = (cc == 1) ? su[1] : sub;
+		sub = (cc == 2) ? su[2] : sub;
+		sub = (cc == 3) ? su[3] : sub;
 		uint32_t cnt = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
 #endif
-		for (int k = 0; k < 8; k++)
-			cnt += dsb_sym2_eq(v[4 + k], pat, within - 32 * k);
+		for (int k = 0; k < 4; k++)
+			cnt += dsb_sym2_eq(v[2 + k], pat, within - 32 * k);
 		if (cc == 0) /* '#' and '$' are stored as 0 */
 			cnt -= spc;
-		return base + cnt;
+		return sub + rel + cnt;
 	}
 	/* '#': line start - A - C - G - T - '$' before the line, then the specials before r that are not '$' */
-	uint64_t start = r & ~255ull;
-	uint64_t h = start - v[0] - v[1] - v[2] - v[3];
+	uint64_t start = r - (uint64_t)within;
+	uint64_t acgt = su[0] + su[1] + su[2] + su[3] + (uint32_t)v[0] + (uint32_t)(v[0] >> 32) + (uint32_t)v[1] +
+			(uint32_t)(v[1] >> 32);
+	uint64_t h = start - acgt;
 	for (int d = 0; d < ix->n_dollar; d++) {
 		if (ix->dollar_row[d] < start)
 			h--;

@@ -40,7 +40,7 @@ static_assert(sizeof(dsb_rstate_t) <= DSB_STATE_BYTES, "per-read phase state mus
 
 /* One phase of classify part A (dsb_phase), one lane per read; the read's control state
  * lives in its workspace between launches.  The last phase publishes the read's summary. */
-template <int PH, bool STATS>
+template <int PH, int STATS>
 __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 					       const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 					       uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t 
 	if (PH != DSB_PH_ISLAND)
 		dsb_state_load(&w, &f, sp);
 	uint64_t st[DSB_ST_N];
-	if (STATS) {
+	if (STATS == 1) {
 		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
 		w.stats = st;
 	}
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t 
 		if (w.overflow)
 			atomicAdd(n_overflow, 1u);
 	}
-	if (STATS)
+	if (STATS == 1)
 		for (int k = 0; k < DSB_ST_N; k++)
 			atomicAdd(gstats + DSB_ST_STRIDE * PH + k, (unsigned long long)st[k]);
 }
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t 
  * the pair exchanges its SEARCH_DIRs.  The reference writes the reverse seeds after the forward
  * ones into one buffer (reverse at L/4, H8): when the forward list runs past L/4 the reverse
  * lane redoes its pass after the forward stores have completed, so its values win there. */
-template <bool STATS>
+template <int STATS>
 __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 							   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 							   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 /* One phase of part A with one wavefront per read (dsb_wave.h), one wave per workgroup:
  * fast seeding (FAST0/FAST1), chaining (RESOLVE_*), scoring (DELA).  The last phase
  * publishes the read's summary like k_phase. */
-template <int PH, bool STATS>
+template <int PH, int STATS>
 __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 						    const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 						    uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
@@ -180,9 +180,16 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 	w.dbg = dbg;
 	w.launch_tag = tag;
 	uint64_t st[DSB_ST_N];
-	if (STATS) {
+	if (STATS == 1) { /* work counters (per lane) */
 		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
 		w.stats = st;
+	}
+	__shared__ uint64_t tmr_lds[DSB_ST_N];
+	if (STATS == 2) { /* wave clocks (lane 0, LDS) */
+		if (lane < DSB_ST_N)
+			tmr_lds[lane] = 0;
+		__syncthreads();
+		w.tmr = tmr_lds;
 	}
 	int active = dsb_phase_active(&w, &f, ph);
 	if (active) {
@@ -231,10 +238,12 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 				atomicAdd(n_overflow, 1u);
 		}
 	}
-	if (STATS)
+	if (STATS == 1)
 		for (int k = 0; k < DSB_ST_N; k++)
 			if (st[k])
 				atomicAdd(gstats + DSB_ST_STRIDE * PH + k, (unsigned long long)st[k]);
+	if (STATS == 2 && lane < DSB_ST_N && tmr_lds[lane])
+		atomicAdd(gstats + DSB_ST_STRIDE * PH + lane, (unsigned long long)tmr_lds[lane]);
 }
 
 

@@ -116,6 +116,7 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 	w->stats = 0;
 	w->dbg = 0;
 	w->launch_tag = 1;
+	w->tmr = 0;
 }
 
 /* glibc chunk-size word in front of the reference's bin_read = realloc(NULL, 2L+20)

@@ -294,6 +294,7 @@ extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
 	/* occ lines (128 B per 256 BWT symbols, re-laid out by the loader) + one zero line */
 	if (upload(g, ix->occ, (ix->n_occ_line + 1) * DSB_OCC_LINE_U64, &h.occ, err, errn)) return -1;
 	h.n_occ_line = ix->n_occ_line;
+	if (upload(g, ix->occ_super, ix->n_occ_super * 4, &h.occ_super, err, errn)) return -1;
 	memcpy(h.dollar_row, ix->dollar_row, sizeof(h.dollar_row));
 	h.n_dollar = ix->n_dollar;
 	memcpy(h.rank, ix->rank, sizeof(h.rank));
@@ -373,12 +374,12 @@ dsb_phase_fn dsb_phase_kernel_7(int wave, int stats);
 dsb_phase_fn dsb_phase_kernel_8(int wave, int stats);
 }
 static_assert(DSB_PH_N == 9, "phase dispatch table");
-static dsb_phase_fn phase_kernel_at(int ph, int wave, bool stats)
+static dsb_phase_fn phase_kernel_at(int ph, int wave, int stats)
 {
 	static dsb_phase_fn (*const get[DSB_PH_N])(int, int) = {
 		dsb_phase_kernel_0, dsb_phase_kernel_1, dsb_phase_kernel_2, dsb_phase_kernel_3, dsb_phase_kernel_4,
 		dsb_phase_kernel_5, dsb_phase_kernel_6, dsb_phase_kernel_7, dsb_phase_kernel_8};
-	return get[ph](wave, stats ? 1 : 0);
+	return get[ph](wave, stats);
 }
 
 static float ev_ms(dsb_gpu_dev *g)
@@ -444,7 +445,7 @@ static uint32_t wave_phases(void)
 }
 
 /* one phase of part A over the reads order[0..m) */
-static void launch_phase(dsb_gpu_dev *g, int ph, bool stats, const uint32_t *cl, uint8_t *wsb, const uint32_t *order,
+static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, uint8_t *wsb, const uint32_t *order,
 			 uint32_t m, hipStream_t s = 0)
 {
 	if (!s)
@@ -590,7 +591,7 @@ static int split_slow(void)
  * reads are split, the scoring of the rest runs on a second stream while the slow phases and
  * then the slow reads' scoring run on the first.  Returns 1 when the rest of part A ran here,
  * 0 when there was nothing to split (the caller continues phase by phase), -1 on error. */
-static int run_split(dsb_gpu_dev *g, bool stats, const uint32_t *cl, uint8_t *wsb, uint32_t cn, dsb_gpu_timing &T,
+static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb, uint32_t cn, dsb_gpu_timing &T,
 		     char *err, size_t errn)
 {
 	hipStream_t s = g->stream;
@@ -724,7 +725,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			hipEventRecord(g->ev_fork, s);
 			HIP_OK(hipStreamWaitEvent(g->stream2, g->ev_fork, 0));
 			hipEventRecord(g->ev_r0, g->stream2);
-			launch_phase(g, DSB_PH_ISLAND, stats_on != 0, cl, wsb, oA, h, g->stream2);
+			launch_phase(g, DSB_PH_ISLAND, stats_on, cl, wsb, oA, h, g->stream2);
 			hipEventRecord(g->ev_r1, g->stream2);
 			if (twB)
 				k_seed<<<(uint32_t)((twB * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
@@ -736,7 +737,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			hipEventElapsedTime(&ms_s, g->ev_a, g->ev_b);
 			T.ms_seed += ms_s;
 			hipEventRecord(g->ev_a, s);
-			launch_phase(g, DSB_PH_ISLAND, stats_on != 0, cl, wsb, oB, cn - h);
+			launch_phase(g, DSB_PH_ISLAND, stats_on, cl, wsb, oB, cn - h);
 			HIP_OK(hipStreamWaitEvent(s, g->ev_r1, 0));
 			float ms_i = ev_ms(g), ms_ia = 0;
 			hipEventElapsedTime(&ms_ia, g->ev_r0, g->ev_r1);
@@ -760,7 +761,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		/* island, fast seeding, resolve: every read */
 		for (int ph = ph0; ph < DSB_PH_N; ph++) {
 			hipEventRecord(g->ev_a, s);
-			launch_phase(g, ph, stats_on != 0, cl, wsb, g->order.as<uint32_t>(), cn);
+			launch_phase(g, ph, stats_on, cl, wsb, g->order.as<uint32_t>(), cn);
 			float ms = ev_ms(g);
 			T.ms_phase[ph] += ms;
 			T.ms_classA += ms;
@@ -768,7 +769,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				T.n_launch_dela++;
 			HIP_OK(hipGetLastError());
 			if (ph == DSB_PH_RESOLVE_F && split_slow()) {
-				int r = run_split(g, stats_on != 0, cl, wsb, cn, T, err, errn);
+				int r = run_split(g, stats_on, cl, wsb, cn, T, err, errn);
 				if (r < 0)
 					return -1;
 				if (r == 1) /* the rest of part A ran split */
@@ -879,7 +880,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			return -1;
 		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
 		hipEventRecord(g->ev_a, s);
-		if (stats_on)
+		if (stats_on == 1)
 			k_classB<true><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
 							 g->order.as<uint32_t>(), cn, g->mrl.as<int32_t>(), g->ro.as<dsb_read_out_t>(),
 							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(), g->stats.as<unsigned long long>());

@@ -23,12 +23,12 @@ extern "C" dsb_phase_fn DSB_CAT(dsb_phase_kernel_, DSB_PH)(int wave, int stats)
 {
 #if DSB_PH == 0
 	(void)wave; /* two lanes per read (k_island); launched with 2 x reads threads */
-	return stats ? k_island<true> : k_island<false>;
+	return stats == 1 ? k_island<1> : (stats == 2 ? k_island<2> : k_island<0>);
 #else
 	if (wave)
-		return stats ? k_wave_phase<DSB_PH, true> : k_wave_phase<DSB_PH, false>;
+		return stats == 1 ? k_wave_phase<DSB_PH, 1> : (stats == 2 ? k_wave_phase<DSB_PH, 2> : k_wave_phase<DSB_PH, 0>);
 #if DSB_LANE_PHASES
-	return stats ? k_phase<DSB_PH, true> : k_phase<DSB_PH, false>;
+	return stats == 1 ? k_phase<DSB_PH, 1> : (stats == 2 ? k_phase<DSB_PH, 2> : k_phase<DSB_PH, 0>);
 #else
 	return nullptr;
 #endif

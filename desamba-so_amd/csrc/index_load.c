@@ -88,32 +88,53 @@ static int occ_relayout(dsb_index *ix, char *err, size_t errn)
 			 (unsigned long)ix->byteLen);
 		return -1;
 	}
-	uint64_t nb = ix->byteLen / 168;
-	ix->n_occ_line = nb;
-	ix->occ = xm((nb + 1) * DSB_OCC_LINE_U64 * 8); /* + one zero line past the end */
-	memset(ix->occ, 0, (nb + 1) * DSB_OCC_LINE_U64 * 8);
+	uint64_t nb = ix->byteLen / 168;          /* file blocks of 256 symbols */
+	uint64_t nl = nb * (256 / DSB_OCC_LINE_SYM); /* HBM lines */
+	ix->n_occ_line = nl;
+	ix->occ = xm((nl + 1) * DSB_OCC_LINE_U64 * 8); /* + one line past the end (occ at r == n) */
+	memset(ix->occ, 0, (nl + 1) * DSB_OCC_LINE_U64 * 8);
+	ix->n_occ_super = ((nl + 1) >> DSB_OCC_SUPER_SHIFT) + 1;
+	ix->occ_super = xm(ix->n_occ_super * 4 * 8);
+	memset(ix->occ_super, 0, ix->n_occ_super * 4 * 8);
 	ix->n_dollar = 0;
-	uint64_t dollars = 0;
+	uint64_t dollars = 0, run[4] = {0, 0, 0, 0};
 	for (uint64_t b = 0; b < nb; b++) {
 		const uint8_t *src = ix->bwt_occ + b * 168;
 		uint64_t cnt[5];
 		memcpy(cnt, src, 40);
-		uint64_t *ln = ix->occ + b * DSB_OCC_LINE_U64;
 		uint64_t hash_before = (b << 8) - cnt[0] - cnt[1] - cnt[2] - cnt[3] - dollars;
 		if (hash_before != cnt[4]) {
 			snprintf(err, errn, "deSAMBA.bwt: block %lu: '#' checkpoint %lu != %lu derived (unexpected occ layout)",
 				 (unsigned long)b, (unsigned long)cnt[4], (unsigned long)hash_before);
 			return -1;
 		}
-		memcpy(ln, cnt, 32);
+		for (int c = 0; c < 4; c++)
+			if (run[c] != cnt[c]) {
+				snprintf(err, errn, "deSAMBA.bwt: block %lu: checkpoint of symbol %d is %lu, %lu counted",
+					 (unsigned long)b, c, (unsigned long)cnt[c], (unsigned long)run[c]);
+				return -1;
+			}
 		for (uint32_t k = 0; k < 256; k++) {
+			uint64_t line = (b << 8 | k) / DSB_OCC_LINE_SYM;
+			uint32_t kk = k % DSB_OCC_LINE_SYM;
+			uint64_t *ln = ix->occ + line * DSB_OCC_LINE_U64;
+			if (kk == 0) { /* line start: counts relative to the superblock */
+				uint64_t *sp = ix->occ_super + (line >> DSB_OCC_SUPER_SHIFT) * 4;
+				if ((line & ((1ull << DSB_OCC_SUPER_SHIFT) - 1)) == 0)
+					memcpy(sp, run, 32);
+				uint32_t rel[4];
+				for (int c = 0; c < 4; c++)
+					rel[c] = (uint32_t)(run[c] - sp[c]);
+				memcpy(ln, rel, 16);
+			}
 			uint64_t w;
 			memcpy(&w, src + 40 + 8 * (k >> 4), 8);
 			uint32_t nib = (uint32_t)((w >> ((k & 15) << 2)) & 0xf);
 			if (nib < 4) {
-				ln[4 + (k >> 5)] |= (uint64_t)nib << (2 * (k & 31));
+				ln[2 + (kk >> 5)] |= (uint64_t)nib << (2 * (kk & 31));
+				run[nib]++;
 			} else {
-				ln[12 + (k >> 6)] |= 1ull << (k & 63);
+				ln[6 + (kk >> 6)] |= 1ull << (kk & 63);
 				if (nib == 5) {
 					if (ix->n_dollar >= DSB_MAX_DOLLAR) {
 						snprintf(err, errn, "deSAMBA.bwt: more than %d '$' symbols (unsupported)", DSB_MAX_DOLLAR);
@@ -124,6 +145,16 @@ static int occ_relayout(dsb_index *ix, char *err, size_t errn)
 				}
 			}
 		}
+	}
+	{ /* the line past the end */
+		uint64_t *ln = ix->occ + nl * DSB_OCC_LINE_U64;
+		uint64_t *sp = ix->occ_super + (nl >> DSB_OCC_SUPER_SHIFT) * 4;
+		if ((nl & ((1ull << DSB_OCC_SUPER_SHIFT) - 1)) == 0)
+			memcpy(sp, run, 32);
+		uint32_t rel[4];
+		for (int c = 0; c < 4; c++)
+			rel[c] = (uint32_t)(run[c] - sp[c]);
+		memcpy(ln, rel, 16);
 	}
 	return 0;
 }
@@ -312,6 +343,7 @@ void dsb_index_free_host_tables(dsb_index *ix)
 {
 	free(ix->bwt_occ); ix->bwt_occ = NULL;
 	free(ix->occ); ix->occ = NULL;
+	free(ix->occ_super); ix->occ_super = NULL;
 	free(ix->hash_index); ix->hash_index = NULL;
 	free(ix->sa); ix->sa = NULL;
 	free(ix->ek0); ix->ek0 = NULL;
@@ -325,6 +357,7 @@ void dsb_index_host_view(const dsb_index *ix, dsb_dindex_t *d)
 {
 	memset(d, 0, sizeof(*d));
 	d->occ = ix->occ; d->n_occ_line = ix->n_occ_line;
+	d->occ_super = ix->occ_super;
 	memcpy(d->dollar_row, ix->dollar_row, sizeof(d->dollar_row)); d->n_dollar = ix->n_dollar;
 	memcpy(d->rank, ix->rank, sizeof(d->rank));
 	d->hash_index = ix->hash_index;

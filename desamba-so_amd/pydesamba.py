@@ -121,7 +121,7 @@ class Index:
         out, n = C.c_void_p(), C.c_uint64(0)
         mrl = C.c_int(max_read_l)
         t = Timing()
-        t.stats_on = 1 if stats else 0
+        t.stats_on = int(stats)  # 1: work counters, 2: wave clocks (DSB_ST_T_*)
         rc = self.L.dsb_classify_text(self.h, data, len(data), fmt, C.byref(mrl), C.byref(out), C.byref(n),
                                       C.byref(t))
         if rc != 0:
@@ -166,7 +166,7 @@ class Batch:
         """Classify every read of the batch; returns the timing dict."""
         mrl = C.c_int(self.max_read_l if max_read_l is None else max_read_l)
         t = Timing()
-        t.stats_on = 1 if stats else 0
+        t.stats_on = int(stats)  # 1: work counters, 2: wave clocks (DSB_ST_T_*)
         if self.L.dsb_batch_run(self.ix.h, self.h, C.byref(mrl), C.byref(t)) != 0:
             raise RuntimeError("dsb_batch_run failed")
         self.max_read_l = mrl.value

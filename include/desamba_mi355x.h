@@ -11,7 +11,7 @@ extern "C" {
 #endif
 
 typedef struct {
-	int stats_on;          /* in: collect algorithmic-work counters (slower kernel variant) */
+	int stats_on;          /* in: 1 collect algorithmic-work counters, 2 wave clocks per code region (slower kernel variants) */
 	int pad;
 	double ms_total;       /* host wall time of the GPU classify call */
 	double ms_h2d, ms_d2h; /* read upload / result download (host-measured) */
