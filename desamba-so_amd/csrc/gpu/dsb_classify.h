@@ -98,6 +98,7 @@ typedef struct {
 	dsb_seed_t *seeds;      /* (L>>1)+20 (+spill) entries; R seeds at L>>2 (src/cly.c:1238,1252) */
 	dsb_anchor_t *anc; uint32_t n_anc;
 	dsb_anchor_t *anc_tmp;
+	dsb_anchor_t *anc_tmp2; /* the seeding state machine's second staging pool (cap.anc entries) */
 	uint32_t *sidx, *stmp;  /* msort permutation scratch (max(anc, hit) entries) */
 	dsb_chain_t *hit; uint32_t n_hit;
 	dsb_chain_t *hit_tmp;
@@ -139,6 +140,8 @@ enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, 
        DSB_ST_T_DPM,    /* sdp_middle predecessor scans */
        DSB_ST_T_DPS,    /* sdp_right / sdp_left predecessor scans */
        DSB_ST_T_FILL,   /* stack-pattern fills of the windows */
+       DSB_ST_PASS2,    /* seeding: seeds run again in the state machine's second pass */
+       DSB_ST_REPLAY,   /* seeding: seeds replayed serially by the whole wave (both passes overflowed) */
        DSB_ST_N };
 /* wave clocks of a code region (timer kernels only: lane 0 accumulates into LDS, so that the
  * timing run pays no private-memory traffic for its counters) */
@@ -1046,7 +1049,6 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	uint32_t lane = dsb_lane();
 	uint32_t n_sv = s_d->l_seed_v_f;
 	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV; /* dbg 32: tiny staging (tests the replay) */
-	dsb_anchor_t *stg = w->anc_tmp + (uint64_t)lane * S;
 	dsb_hset_t hs = {hset + DSB_HSET_SLOT_U64 * lane, DSB_HSET_SLOT_U64 * DSB_WV, 0, 0, 500,
 			 dsb_hset_tag(w)};
 	uint8_t l_ek = (uint8_t)ix->l_ek;
@@ -1058,7 +1060,9 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	int n_top = 0, total = 0;
 	uint8_t *bin_read = w->bin + (s_d->strand ? w->L : 0);
 	/* ---- top seeds, in order (tix) */
-	uint32_t *tix = w->sidx, *rec = w->hh[0]; /* records: the read-hash region is free while seeding */
+	/* the read-hash region is free while seeding (>= 16 L bytes; n_sv <= L/3 + 1): 2 record words,
+	 * the pass-1 list and the top-seed list per seed */
+	uint32_t *rec = w->hh[0], *klist = rec + 2 * (uint64_t)n_sv, *tix = rec + 3 * (uint64_t)n_sv;
 	uint32_t m = 0;
 	for (uint32_t gb = 0; gb < n_sv; gb += DSB_WV) {
 		uint32_t ci = gb + lane;
@@ -1075,21 +1079,35 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 			w->fast_classify = 0;
 		return;
 	}
-	/* ---- the lane's anchor vector is its staging area while seeds run */
 	dsb_anchor_t *anc0 = w->anc;
 	uint32_t n0 = w->n_anc, cap0 = w->cap.anc, of0 = w->overflow;
-	w->anc = stg;
-	w->n_anc = 0;
-	w->cap.anc = S;
-	w->overflow = 0;
 	/* ---- per-lane seed state; every record starts as "overflowed" (replayed if never written) */
 	for (uint32_t q = lane; q < m; q += DSB_WV) {
 		rec[2 * q] = 0;
 		rec[2 * q + 1] = 1u << 30;
 	}
 	dsb_wsync();
-	uint32_t next_k = DSB_MIN((uint32_t)DSB_WV, m); /* next top seed to hand out (uniform) */
-	uint32_t k = lane;                                /* my top-seed index */
+	/* Two passes.  Pass 0 hands every top seed out; a lane's anchors go to its 1/64 slice of the
+	 * staging pool (anc_tmp) and a lane whose slice fills retires, leaving its seed (and the seeds
+	 * never handed out) flagged overflowed.  Pass 1 runs those seeds again with a second pool
+	 * (anc_tmp2) split over only as many lanes as there are such seeds, so one seed of a repeat
+	 * region with hundreds of anchors still runs on the state machine instead of the serial
+	 * replay of the compaction below (which stays for what overflows both). */
+	uint32_t n_ovf = 0, S2 = S;
+	for (uint32_t pr = 0; pr < 2; pr++) {
+	uint32_t mp = pr ? n_ovf : m;
+	if (mp == 0)
+		break;
+	uint32_t Sp = pr ? S2 : S;
+	dsb_anchor_t *pool = pr ? w->anc_tmp2 : w->anc_tmp;
+	/* ---- the lane's anchor vector is its staging area while seeds run */
+	dsb_anchor_t *stg = pool + (uint64_t)lane * Sp;
+	w->anc = stg;
+	w->n_anc = 0;
+	w->cap.anc = Sp;
+	w->overflow = 0;
+	uint32_t next_k = DSB_MIN((uint32_t)DSB_WV, mp); /* next seed of the pass to hand out (uniform) */
+	uint32_t k = lane;                                 /* my top-seed index */
 	int st = DSB_SM_DONE;
 	uint32_t ci = 0, a_b = 0, seed_off = 0;
 	int j = 0, skip = 0, n_m = 0, k_map = 0, max_score = 0, string_index = 0, match_len = 0, row_single = 0;
@@ -1102,7 +1120,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	}
 #define DSB_SM_START_SEED(K)                                                   \
 	do {                                                                   \
-		k = (K);                                                       \
+		k = pr ? klist[K] : (K);                                       \
 		ci = tix[k];                                                   \
 		const dsb_seed_t *c_sv_ = w->seeds + s_d->seed_off + ci;       \
 		seed_off = c_sv_->offset;                                      \
@@ -1113,6 +1131,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 		a_b = w->n_anc;                                                \
 		dsb_set_reset(&hs);                                            \
 		st = DSB_SM_J;                                                 \
+		DSB_EMU_PROF_START();                                          \
 	} while (0)
 	/* a finished single search: fast keeps hits >= L_MIN in m_r (src/cly.c:1424-1426); slow keeps a
 	 * stable top 8 by match length of all hits of the seed (the qsort of src/cly.c:1590) */
@@ -1137,13 +1156,22 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 			}                                                                      \
 		}                                                                              \
 	} while (0)
-	if (k < m)
+#ifdef DSB_EMU_PROF /* test-only emulator profile (tests/emu): trips of the state machine per seed */
+	uint64_t prof_trips = 0, prof_maps = 0;
+#define DSB_EMU_PROF_START() (prof_trips = 0, prof_maps = 0)
+#else
+#define DSB_EMU_PROF_START() ((void)0)
+#endif
+	if (lane < mp)
 		DSB_SM_START_SEED(lane);
 	uint64_t t_sm = DSB_T0();
 	for (;;) {
 		uint64_t act = dsb_wballot(st != DSB_SM_DONE);
 		if (!act)
 			break;
+#ifdef DSB_EMU_PROF
+		prof_trips++;
+#endif
 		uint64_t mapm = dsb_wballot(st == DSB_SM_MAP);
 		int do_map = mapm != 0 && ((uint32_t)__builtin_popcountll(mapm) >= DSB_SM_MAP_BATCH || mapm == act);
 		if (w->stats && lane == 0) { /* trip counters (stats kernels): trips, map trips, lanes mapping */
@@ -1220,8 +1248,8 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 				uint32_t start = opfx > cb ? opfx - cb : 0; /* the owner's first item in this chunk */
 				uint64_t before = (lane == 0 ? 0 : (~0ull >> (64 - lane))) & ~(start == 0 ? 0 : (~0ull >> (64 - start)));
 				uint32_t dest = o_n + (uint32_t)__builtin_popcountll(pm & before);
-				if (pass && dest < S) {
-					w->anc_tmp[(uint64_t)o * S + dest] = an;
+				if (pass && dest < Sp) {
+					pool[(uint64_t)o * Sp + dest] = an;
 					if (w->stats) w->stats[DSB_ST_ANCHOR]++;
 				}
 				if (pass)
@@ -1239,15 +1267,18 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 			if (inmap) {
 				int c_score = cx.ret;
 				if (cx.n_items) { /* max over the kept anchors (the reference's max_s) */
-					if (n_before > S) {
+					if (n_before > Sp) {
 						w->overflow |= 1;
-						n_before = S;
+						n_before = Sp;
 					}
 					c_score = omax[lane];
 					w->n_anc = n_before;
 				}
 				max_score = DSB_MAX(c_score, max_score);
 				k_map++;
+#ifdef DSB_EMU_PROF
+				prof_maps++;
+#endif
 			}
 			DSB_T1(DSB_ST_T_MAP, t1); /* lane 0: wave clocks in the batched map steps */
 		}
@@ -1393,7 +1424,10 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 				for (uint32_t a = a_b; a < w->n_anc; a++)
 					stg[a].anchor_useless = (stg[a].score < top_score) ? 1 : 0;
 			}
-			rec[2 * k] = (lane << 24) | a_b;
+#ifdef DSB_EMU_PROF
+			dsb_emu_prof_seed(SLOW, k, prof_trips, prof_maps);
+#endif
+			rec[2 * k] = (pr << 31) | (lane << 24) | a_b;
 			rec[2 * k + 1] = ((uint32_t)(!SLOW && skip && !w->overflow) << 31) | ((uint32_t)(w->overflow != 0) << 30) |
 					 (w->overflow ? 0u : (w->n_anc - a_b));
 		}
@@ -1404,7 +1438,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 			uint32_t mine = next_k + (uint32_t)__builtin_popcountll(below);
 			next_k += (uint32_t)__builtin_popcountll(finm);
 			if (st == DSB_SM_FIN) {
-				if (w->overflow || mine >= m)
+				if (w->overflow || mine >= mp)
 					st = DSB_SM_DONE; /* an overflowed lane's staging is full: it retires */
 				else
 					DSB_SM_START_SEED(mine);
@@ -1439,7 +1473,24 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	DSB_T1(DSB_ST_T_MEM, t_sm); /* lane 0: wave clocks in the whole state machine */
 #undef DSB_SM_START_SEED
 #undef DSB_SM_KEEP
+#undef DSB_EMU_PROF_START
 	dsb_wsync();
+	if (pr == 0) { /* the seeds pass 1 runs again: records still flagged overflowed, in order */
+		for (uint32_t gb = 0; gb < m; gb += DSB_WV) {
+			uint32_t kk = gb + lane;
+			int o = kk < m && ((rec[2 * kk + 1] >> 30) & 1);
+			uint64_t bm = dsb_wballot(o);
+			uint64_t below = (lane == 0) ? 0 : (bm & (~0ull >> (64 - lane)));
+			if (o)
+				klist[n_ovf + (uint32_t)__builtin_popcountll(below)] = kk;
+			n_ovf += (uint32_t)__builtin_popcountll(bm);
+		}
+		dsb_wsync();
+		if (n_ovf && w->stats && lane == 0)
+			w->stats[DSB_ST_PASS2] += n_ovf;
+		S2 = (w->dbg & 32) ? 2 : cap0 / DSB_MIN((uint32_t)DSB_WV, DSB_MAX(n_ovf, 1u));
+	}
+	} /* passes */
 	w->anc = anc0;
 	w->n_anc = n0;
 	w->cap.anc = cap0;
@@ -1454,7 +1505,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 		uint32_t cix = act ? tix[kk] : 0;
 		uint32_t r0 = act ? rec[2 * kk] : 0, r1 = act ? rec[2 * kk + 1] : 0;
 		int trig = (int)(r1 >> 31), ovf = (int)((r1 >> 30) & 1);
-		uint32_t cnt = r1 & 0x3fffffffu, src_lane = r0 >> 24, src_off = r0 & 0xffffffu;
+		uint32_t cnt = r1 & 0x3fffffffu, src_lane = (r0 >> 24) & 0x7fu, src_off = r0 & 0xffffffu, pool_ = r0 >> 31;
 		uint64_t tm = dsb_wballot(act && trig);
 		uint64_t om = dsb_wballot(act && ovf);
 		uint64_t skipm = 0;
@@ -1484,7 +1535,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 				dsb_wsync();
 				return;
 			}
-			const dsb_anchor_t *src = w->anc_tmp + (uint64_t)src_lane * S + src_off;
+			const dsb_anchor_t *src = (pool_ ? w->anc_tmp2 + (uint64_t)src_lane * S2 : w->anc_tmp + (uint64_t)src_lane * S) + src_off;
 			for (uint32_t e = 0; e < cnt; e++)
 				w->anc[w->n_anc + off + e] = src[e];
 			w->n_anc += tot;
@@ -1496,6 +1547,8 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 					continue;
 				}
 				if ((om >> q) & 1) { /* replay on every lane, straight into the anchor vector */
+					if (w->stats && lane == 0)
+						w->stats[DSB_ST_REPLAY]++;
 					if (SLOW) {
 						dsb_slow_seed(w, s_d, cq, &hs, top);
 						last_trig = 0;
@@ -1514,7 +1567,8 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 						dsb_wsync();
 						return;
 					}
-					const dsb_anchor_t *src = w->anc_tmp + (uint64_t)sl * S + so;
+					uint32_t sp_ = (uint32_t)dsb_wshfl((int)pool_, (int)q);
+					const dsb_anchor_t *src = (sp_ ? w->anc_tmp2 + (uint64_t)sl * S2 : w->anc_tmp + (uint64_t)sl * S) + so;
 					for (uint32_t e = lane; e < kc; e += DSB_WV)
 						w->anc[w->n_anc + e] = src[e];
 					w->n_anc += kc;

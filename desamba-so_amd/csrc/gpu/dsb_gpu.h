@@ -15,6 +15,12 @@ extern "C" {
 #define DSB_MAX_HITS 400 /* delete_small_score_rst keeps at most 400 chains (src/cly.c:2892) */
 
 #define DSB_ST_STRIDE 32 /* counters per phase */
+/* DSB_WAVE_DBG bit: per-read wall-clock timeline of the wave phases (dev tool: a DSB_TL=1 build,
+ * DSB_TIMELINE=path):
+ * record {start, end, read | phase << 32, hw_id} of slot t of phase ph at
+ * stats[DSB_N_STATS + 4 * (ph * DSB_TL_STRIDE + t)] (s_memrealtime, 100 MHz) */
+#define DSB_DBG_TIMELINE (1u << 12)
+#define DSB_TL_STRIDE (1u << 17)
 #define DSB_N_STATS 320 /* 32 counters x (9 phases of part A + k_classB) */
 #define DSB_STATS_B 288
 

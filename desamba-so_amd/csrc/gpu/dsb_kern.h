@@ -35,6 +35,10 @@
 #ifndef DSB_WIN_IN_LDS
 #define DSB_WIN_IN_LDS 1
 #endif
+/* DSB_TL=1 (dev builds, tools/variant.sh): the per-read timeline of DSB_DBG_TIMELINE */
+#ifndef DSB_TL
+#define DSB_TL 0
+#endif
 #define DSB_DELA_LDS_BYTES (DSB_WIN_LDS_BYTES + 64 > DSB_HB_LDS ? DSB_WIN_LDS_BYTES + 64 : DSB_HB_LDS)
 static_assert(sizeof(dsb_rstate_t) <= DSB_STATE_BYTES, "per-read phase state must fit its workspace slot");
 
@@ -151,23 +155,21 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 		dsb_state_save(&w, &f, sp);
 }
 
-/* One phase of part A with one wavefront per read (dsb_wave.h), one wave per workgroup:
- * fast seeding (FAST0/FAST1), chaining (RESOLVE_*), scoring (DELA).  The last phase
- * publishes the read's summary like k_phase. */
+/* One read of a phase of part A with one wavefront per read (dsb_wave.h): fast seeding
+ * (FAST0/FAST1), chaining (RESOLVE_*), scoring (DELA).  The last phase publishes the read's
+ * summary like k_phase. */
 template <int PH, int STATS>
-__global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
-						    const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
-						    uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
-						    dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
-						    unsigned long long *__restrict__ gstats, uint32_t dbg,
-									      uint32_t tag)
+__device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+						const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+						uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t t,
+						dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
+						uint64_t *st, uint64_t *tmr_lds, unsigned long long *__restrict__ gstats,
+						uint32_t dbg, uint32_t tag)
 {
 	const int ph = PH;
-	uint32_t t = blockIdx.x;
-	if (t >= n)
-		return;
 	uint32_t lane = threadIdx.x;
 	uint32_t r = order[t];
+	uint64_t tl0 = (DSB_TL && (dbg & DSB_DBG_TIMELINE)) ? __builtin_amdgcn_s_memrealtime() : 0;
 	uint32_t L = len[r];
 	uint8_t *base = ws + ws_off[r];
 	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
@@ -179,18 +181,10 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 	dsb_state_load(&w, &f, sp);
 	w.dbg = dbg;
 	w.launch_tag = tag;
-	uint64_t st[DSB_ST_N];
-	if (STATS == 1) { /* work counters (per lane) */
-		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
+	if (STATS == 1)
 		w.stats = st;
-	}
-	__shared__ uint64_t tmr_lds[DSB_ST_N];
-	if (STATS == 2) { /* wave clocks (lane 0, LDS) */
-		if (lane < DSB_ST_N)
-			tmr_lds[lane] = 0;
-		__syncthreads();
+	if (STATS == 2)
 		w.tmr = tmr_lds;
-	}
 	int active = dsb_phase_active(&w, &f, ph);
 	if (active) {
 		if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
@@ -238,6 +232,39 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 				atomicAdd(n_overflow, 1u);
 		}
 	}
+	if (DSB_TL && (dbg & DSB_DBG_TIMELINE) && lane == 0 && t < DSB_TL_STRIDE) {
+		unsigned long long *e = gstats + DSB_N_STATS + 4ull * (PH * DSB_TL_STRIDE + t);
+		e[0] = tl0;
+		e[1] = __builtin_amdgcn_s_memrealtime();
+		e[2] = r | ((unsigned long long)PH << 32) | ((unsigned long long)active << 40);
+		e[3] = __builtin_amdgcn_s_getreg(4 | (31 << 11)) | /* HW_ID (wave, SIMD, CU, SE), XCC_ID */
+		       ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+	}
+}
+
+/* A phase of part A, one wave per workgroup: workgroup t runs read order[t]. */
+template <int PH, int STATS>
+__global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+						    const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+						    uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+						    dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
+						    unsigned long long *__restrict__ gstats, uint32_t dbg,
+									      uint32_t tag)
+{
+	uint32_t lane = threadIdx.x;
+	uint64_t st[DSB_ST_N];
+	if (STATS == 1) /* work counters (per lane) */
+		for (int k = 0; k < DSB_ST_N; k++) st[k] = 0;
+	__shared__ uint64_t tmr_lds[DSB_ST_N];
+	if (STATS == 2) { /* wave clocks (lane 0, LDS) */
+		if (lane < DSB_ST_N)
+			tmr_lds[lane] = 0;
+		__syncthreads();
+	}
+	uint32_t t = blockIdx.x;
+	if (t >= n)
+		return;
+	wave_phase_read<PH, STATS>(ix, len, ws_off, scale, ws, order, t, ro, n_overflow, st, tmr_lds, gstats, dbg, tag);
 	if (STATS == 1)
 		for (int k = 0; k < DSB_ST_N; k++)
 			if (st[k])

@@ -40,7 +40,7 @@ DSB_HD uint32_t dsb_ex_words(uint32_t L) { return (L >> 6) + 2; }
 DSB_HD uint32_t dsb_seed_cap(uint32_t L) { return (L >> 1) + 20 + L / 3 + 64; }
 
 typedef struct {
-	uint64_t bin, exF, exR, pre, seeds, anc, anc_tmp, sidx, stmp, hit, hit_tmp, sms, hash, sch, win, mem, spset, hset, state, total;
+	uint64_t bin, exF, exR, pre, seeds, anc, anc_tmp, anc_tmp2, sidx, stmp, hit, hit_tmp, sms, hash, sch, win, mem, spset, hset, state, total;
 	uint32_t kl;
 } dsb_ws_layout;
 
@@ -56,6 +56,7 @@ DSB_HD dsb_ws_layout dsb_layout(uint32_t L, dsb_caps_t cap)
 	o.seeds = p; p = dsb_al(p + sizeof(dsb_seed_t) * (uint64_t)dsb_seed_cap(L));
 	o.anc = p; p = dsb_al(p + sizeof(dsb_anchor_t) * (uint64_t)cap.anc);
 	o.anc_tmp = p; p = dsb_al(p + DSB_MAX(sizeof(dsb_anchor_t) * (uint64_t)cap.anc, sizeof(dsb_mem_t) * 256ull));
+	o.anc_tmp2 = p; p = dsb_al(p + sizeof(dsb_anchor_t) * (uint64_t)cap.anc);
 	o.sidx = p; p = dsb_al(p + 4ull * sortn);
 	o.stmp = p; p = dsb_al(p + 4ull * sortn);
 	o.hit = p; p = dsb_al(p + sizeof(dsb_chain_t) * (uint64_t)cap.hit);
@@ -87,6 +88,7 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 	w->anc = (dsb_anchor_t *)(base + o.anc);
 	w->n_anc = 0;
 	w->anc_tmp = (dsb_anchor_t *)(base + o.anc_tmp);
+	w->anc_tmp2 = (dsb_anchor_t *)(base + o.anc_tmp2);
 	w->sidx = (uint32_t *)(base + o.sidx);
 	w->stmp = (uint32_t *)(base + o.stmp);
 	w->hit = (dsb_chain_t *)(base + o.hit);

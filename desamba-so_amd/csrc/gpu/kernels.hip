@@ -579,11 +579,15 @@ static int split_seed(void)
 	return v;
 }
 
+/* The split of part A (run_split) is off by default: with the slow reads' seeds no longer
+ * replayed serially, the slow phases take ~9 ms in a row, while beside the scoring grid their
+ * workgroups wait for its waves to free CUs (measured r02: 564k vs 555k reads/s).  DSB_SPLIT=1
+ * turns it on. */
 static int split_slow(void)
 {
 	static int v = -1;
 	if (v < 0)
-		v = getenv("DSB_NO_SPLIT") ? 0 : 1;
+		v = getenv("DSB_SPLIT") ? 1 : 0;
 	return v;
 }
 
@@ -655,9 +659,13 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		return 0;
 	if (g->scale.ensure(4 * n + 4, err, errn) || g->ro.ensure(sizeof(dsb_read_out_t) * n + 64, err, errn) ||
 	    g->mrl.ensure(4 * n + 4, err, errn) || g->hit_off.ensure(4 * n + 4, err, errn) ||
-	    g->cnt.ensure(64, err, errn) || g->stats.ensure(8 * DSB_N_STATS, err, errn) || g->ws_off.ensure(8 * n + 8, err, errn))
+	    g->cnt.ensure(64, err, errn) || g->ws_off.ensure(8 * n + 8, err, errn))
 		return -1;
-	HIP_OK(hipMemsetAsync(g->stats.p, 0, 8 * DSB_N_STATS, s));
+	/* DSB_DBG_TIMELINE (dev tool, DSB_TIMELINE=path): per-read phase timeline after the counters */
+	const size_t tl_bytes = (wave_dbg() & DSB_DBG_TIMELINE) ? 8ull * 4 * DSB_PH_N * DSB_TL_STRIDE : 0;
+	if (g->stats.ensure(8 * DSB_N_STATS + tl_bytes, err, errn))
+		return -1;
+	HIP_OK(hipMemsetAsync(g->stats.p, 0, 8 * DSB_N_STATS + tl_bytes, s));
 	/* DSB_TEST_SCALE0 (tests): start below the default capacities so that reads overflow and
 	 * take the re-run path */
 	uint32_t scale0 = DSB_SCALE_UNIT;
@@ -905,6 +913,14 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		cb = ce;
 	}
 	*max_read_l = carry;
+	if (tl_bytes && getenv("DSB_TIMELINE")) {
+		std::vector<uint64_t> tl(tl_bytes / 8);
+		HIP_OK(hipMemcpy(tl.data(), g->stats.as<uint8_t>() + 8 * DSB_N_STATS, tl_bytes, hipMemcpyDeviceToHost));
+		if (FILE *f = fopen(getenv("DSB_TIMELINE"), "wb")) {
+			fwrite(tl.data(), 8, tl.size(), f);
+			fclose(f);
+		}
+	}
 	if (stats_on) {
 		unsigned long long st[DSB_N_STATS];
 		HIP_OK(hipMemcpy(st, g->stats.p, sizeof(st), hipMemcpyDeviceToHost));

@@ -13,6 +13,15 @@
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
+#ifdef DSB_EMU_PROF /* emu_prof: per-seed state-machine trips (tools/seed_prof.py) */
+#include <stdint.h>
+struct emu_prof_seed { uint32_t k; uint64_t trips, maps; };
+static std::vector<emu_prof_seed> g_prof[2];
+static void dsb_emu_prof_seed(int slow, uint32_t k, uint64_t trips, uint64_t maps)
+{
+	g_prof[slow ? 1 : 0].push_back({k, trips, maps});
+}
+#endif
 extern "C" {
 #include "../../desamba-so_amd/csrc/dsb_host.h"
 }
@@ -123,6 +132,17 @@ int main(int argc, char **argv)
 				dsb_phase<true>(&w, &f, DSB_PH_DELA);
 			} else
 				dsb_classify_A(&w);
+#ifdef DSB_EMU_PROF
+			if (scale == DSB_SCALE_UNIT) {
+				printf("R %lu %u", (unsigned long)i, L);
+				for (int sl = 0; sl < 2; sl++) {
+					printf(" %s", sl ? "|S" : "|F");
+					for (const emu_prof_seed &q : g_prof[sl]) printf(" %lu,%lu", (unsigned long)q.trips, (unsigned long)q.maps);
+					g_prof[sl].clear();
+				}
+				printf("\n");
+			}
+#endif
 			if (getenv("DSB_DEBUG_READ") && strtoull(getenv("DSB_DEBUG_READ"), 0, 10) == i)
 				dsb_debug_dump(stderr, &w, "emuA");
 			if (w.overflow) {
@@ -135,7 +155,9 @@ int main(int argc, char **argv)
 			max_read_l = mrl;
 			break;
 		}
+#ifndef DSB_EMU_PROF
 		dsb_format_read(&out, &ix, &reads, i, &ro, hits.data(), fmt, 5);
+#endif
 		if (out.l > (1 << 24)) {
 			fwrite(out.s, 1, out.l, stdout);
 			out.l = 0;
