@@ -208,10 +208,13 @@ def main():
     cdev = "cuda" if (dist is None or dist.get_backend() == "nccl") else "cpu"
     counts = torch.zeros(n_tax, dtype=torch.int64, device=cdev)
 
+    dev_counts = torch.zeros(n_tax, dtype=torch.int64, device="cuda")
+
     def step():
         tm = batch.run(max_read_l=0)
-        tid, _ = batch.taxa(0)
-        counts.copy_(shard.reduce_counts(shard.taxon_counts(tid, None, n_tax, cdev), cdev))
+        # per-read taxa (computed by the classify kernels) reduced to per-taxon counts on the GPU
+        batch.taxon_counts(dev_counts, 0)
+        counts.copy_(shard.reduce_counts(dev_counts if cdev == "cuda" else dev_counts.cpu(), cdev))
         return tm
 
     for _ in range(a.warmup):

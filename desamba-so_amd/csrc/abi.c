@@ -59,6 +59,9 @@ void load_index(void **idx, const char *dirPath)
 	ix->ref_tid = malloc(sizeof(uint32_t) * (ix->n_ref + 1));
 	for (uint64_t r = 0; r < ix->n_ref; r++)
 		ix->ref_tid[r] = name_taxid(ix->ref_name[r]);
+	ix->p_tid = malloc(sizeof(uint32_t) * (ix->max_tid + 1));
+	for (uint64_t t = 0; t <= ix->max_tid; t++)
+		ix->p_tid[t] = ix->tax[t].p_tid;
 	if (dsb_gpu_init(ix, -1, err, sizeof(err))) fatal("load_index", err);
 	if (!getenv("DSB_KEEP_HOST_TABLES"))
 		dsb_index_free_host_tables(ix);
@@ -268,39 +271,32 @@ int dsb_batch_taxa(void *idx, dsb_batch *b, int flag, uint32_t *tid_out, uint64_
 	dsb_index *ix = idx;
 	const dsb_read_out_t *ro = dsb_gpu_batch_ro(b->g);
 	const dsb_hit_out_t *hits = dsb_gpu_batch_hits(b->g);
-	uint32_t *rec_tid = malloc(sizeof(uint32_t) * (DSB_MAX_HITS + 1));
-	uint32_t *rec_score = malloc(sizeof(uint32_t) * (DSB_MAX_HITS + 1));
 	for (uint64_t i = 0; i < b->reads.n; i++) {
 		const dsb_rec_t *rec = b->reads.rec + i;
 		/* the SAM text meta_analysis parses prints SEQ with %s: its length is strlen */
 		weight_out[i] = (flag & 1) ? (uint64_t)strlen(b->reads.arena + rec->seq_off) : 1;
-		uint32_t nh = ro[i].n_hit;
-		if (nh == 0) { tid_out[i] = 0; continue; }
-		const dsb_hit_out_t *h = hits + ro[i].hit_off;
-		/* SAM record order of output_one_result_sam: primary, supplementaries, secondaries */
-		uint32_t nr = 0;
-		rec_tid[nr] = ix->ref_tid[h[0].ref_ID]; rec_score[nr++] = h[0].sum_score;
-		for (int loop = 0; loop <= 1; loop++)
-			for (uint32_t k = 1; k < nh; k++)
-				if ((loop == 0 && h[k].pri_index == 0) || (loop == 1 && h[k].pri_index > 0 && h[k].pri_index <= 5)) {
-					rec_tid[nr] = ix->ref_tid[h[k].ref_ID];
-					rec_score[nr++] = h[k].sum_score;
-				}
-		/* ana_get_tid: an equal-score later record of a descendant taxon wins */
-		uint32_t tid = 0, score = 0;
-		if (rec_tid[0] <= ix->max_tid) { tid = rec_tid[0]; score = rec_score[0]; }
-		for (uint32_t k = 1; k < nr && score != 0; k++) {
-			if (rec_score[k] != score || rec_tid[k] > ix->max_tid) continue;
-			for (uint32_t pt = rec_tid[k];; pt = ix->tax[pt].p_tid) {
-				if (pt == tid) { tid = rec_tid[k]; break; }
-				if (pt < 1 || pt == 4294967295u) break;
-			}
-		}
-		tid_out[i] = tid;
+		tid_out[i] = dsb_read_taxon(hits + ro[i].hit_off, ro[i].n_hit, ix->ref_tid, ix->p_tid, ix->max_tid);
 	}
-	free(rec_tid);
-	free(rec_score);
 	return 0;
+}
+
+int dsb_batch_taxon_counts(void *idx, dsb_batch *b, int flag, uint64_t *dev_counts, uint64_t n_counts)
+{
+	dsb_index *ix = idx;
+	char err[512];
+	if (n_counts < ix->max_tid + 1)
+		return -1;
+	uint32_t *w = NULL;
+	if (flag & 1) { /* strlen of each SEQ, as meta_analysis' parse of the SAM text sees it */
+		w = malloc(sizeof(uint32_t) * (b->reads.n + 1));
+		for (uint64_t i = 0; i < b->reads.n; i++)
+			w[i] = (uint32_t)strlen(b->reads.arena + b->reads.rec[i].seq_off);
+	}
+	int rc = dsb_gpu_batch_counts(ix, b->g, w, dev_counts, n_counts, err, sizeof(err));
+	free(w);
+	if (rc)
+		fprintf(stderr, "[dsb] dsb_batch_taxon_counts: %s\n", err);
+	return rc;
 }
 
 int dsb_batch_carry(dsb_batch *b, int32_t *carry_out)
@@ -345,7 +341,7 @@ void dsb_unload_index(void *idx)
 	if (!ix) return;
 	dsb_gpu_free(ix);
 	dsb_index_free_host_tables(ix);
-	free(ix->Q_MEM); free(ix->ref_name); free(ix->ref_tid); free(ix->ref_seq_l); free(ix->ref_seq_offset); free(ix->tax);
+	free(ix->Q_MEM); free(ix->ref_name); free(ix->ref_tid); free(ix->p_tid); free(ix->ref_seq_l); free(ix->ref_seq_offset); free(ix->tax);
 	struct dsb_thread_state *s = ix->states;
 	while (s) { struct dsb_thread_state *n = s->next; free(s); s = n; }
 	pthread_mutex_destroy(&ix->state_mutex);

@@ -40,6 +40,7 @@ typedef struct dsb_index {
 	uint64_t n_ref;
 	char (*ref_name)[128];
 	uint32_t *ref_tid;        /* taxid of each reference name ("tid|<taxid>|...", cly_mt.c:778-786) */
+	uint32_t *p_tid;          /* parent taxid per taxid (tax[].p_tid), max_tid + 1 entries */
 	uint64_t *ref_seq_l, *ref_seq_offset;
 	uint64_t *r_p; uint64_t n_rp;
 	int *Q_MEM;               /* DSB_Q_MEM_PAD */

@@ -71,6 +71,11 @@ typedef struct {
 	const int *Q_MEM;            /* DSB_Q_MEM_PAD ints */
 	const int *Q_LV;             /* [20][20] row-major: Q_LV[ed*20 + len] */
 	int filter_min_length, filter_min_score, filter_min_score_LV3;
+	/* taxonomy for the per-read taxon (meta_analysis' ana_get_tid): taxid of each reference and
+	 * parent taxid of every taxid <= max_tid (0xffffffff: none) */
+	const uint32_t *ref_tid;
+	const uint32_t *p_tid;
+	uint64_t max_tid;
 } dsb_dindex_t;
 
 /* Output record per hit (what output_one_result_sam needs, cly_mt.c:229-327) */
@@ -81,6 +86,49 @@ typedef struct {
 	uint32_t indel;
 	uint8_t direction, primary, pri_index, pad;
 } dsb_hit_out_t;
+
+/*
+ * The taxon meta_analysis assigns a read from its records (ana_get_tid, reference
+ * src/cly_mt.c:902-961), taken from the hits in the order output_one_result_sam prints them
+ * (src/cly_mt.c:229-327: primary, supplementaries (pri_index 0), secondaries (pri_index 1..5)):
+ * the first record's taxid, replaced by a later record of equal score whose taxid descends from
+ * the current one.  0 = unclassified.  Shared by the host (dsb_batch_taxa) and the classB kernel.
+ */
+#if defined(__HIPCC__)
+#define DSB_TAX_HD __host__ __device__ static inline
+#else
+#define DSB_TAX_HD static inline
+#endif
+DSB_TAX_HD uint32_t dsb_read_taxon(const dsb_hit_out_t *h, uint32_t nh, const uint32_t *ref_tid, const uint32_t *p_tid,
+				   uint64_t max_tid)
+{
+	if (nh == 0)
+		return 0;
+	uint32_t tid = 0, score = 0;
+	uint32_t t0 = ref_tid[h[0].ref_ID];
+	if (t0 <= max_tid) {
+		tid = t0;
+		score = h[0].sum_score;
+	}
+	for (int loop = 0; loop <= 1 && score != 0; loop++)
+		for (uint32_t k = 1; k < nh && score != 0; k++) {
+			int printed = loop == 0 ? h[k].pri_index == 0 : (h[k].pri_index > 0 && h[k].pri_index <= 5);
+			if (!printed || h[k].sum_score != score)
+				continue;
+			uint32_t rt = ref_tid[h[k].ref_ID];
+			if (rt > max_tid)
+				continue;
+			for (uint32_t pt = rt;; pt = p_tid[pt]) {
+				if (pt == tid) {
+					tid = rt;
+					break;
+				}
+				if (pt < 1 || pt == 4294967295u || pt > max_tid)
+					break;
+			}
+		}
+	return tid;
+}
 
 /* Per-read result summary */
 typedef struct {

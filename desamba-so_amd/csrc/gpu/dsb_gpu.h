@@ -59,6 +59,10 @@ const int32_t *dsb_gpu_batch_carry(const dsb_gpu_batch *b);
 uint64_t dsb_gpu_batch_n(const dsb_gpu_batch *b);
 uint64_t dsb_gpu_batch_bases(const dsb_gpu_batch *b);
 void dsb_gpu_batch_free(dsb_index *ix, dsb_gpu_batch *b);
+/* per-taxon weights of the last run into dev_counts[0, n_counts) on the index's GPU (zeroed
+ * first): the per-read taxa come from classB (dsb_read_taxon); weights[i] (host, NULL = 1) */
+int dsb_gpu_batch_counts(dsb_index *ix, dsb_gpu_batch *b, const uint32_t *weights, uint64_t *dev_counts,
+			 uint64_t n_counts, char *err, size_t errn);
 
 /* Number of visible devices (0 if HIP has none). */
 int dsb_gpu_device_count(void);

@@ -116,7 +116,8 @@ __global__ __launch_bounds__(64) void k_classB(const dsb_dindex_t *__restrict__ 
 						uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 						const int32_t *__restrict__ mrl, dsb_read_out_t *__restrict__ ro,
 						dsb_hit_out_t *__restrict__ hits_out, uint32_t *__restrict__ hit_cursor,
-						uint32_t *__restrict__ hit_off, unsigned long long *__restrict__ gstats)
+						uint32_t *__restrict__ hit_off, uint32_t *__restrict__ tid_out,
+						unsigned long long *__restrict__ gstats)
 {
 	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= n)
@@ -145,9 +146,19 @@ __global__ __launch_bounds__(64) void k_classB(const dsb_dindex_t *__restrict__ 
 	hit_off[r] = off;
 	o.hit_off = off;
 	ro[r] = o;
+	tid_out[r] = dsb_read_taxon(stage, o.n_hit, ix->ref_tid, ix->p_tid, ix->max_tid);
 	if (STATS)
 		for (int k = 0; k < DSB_ST_N; k++)
 			atomicAdd(gstats + DSB_STATS_B + k, (unsigned long long)st[k]);
+}
+
+/* per-taxon weights (meta_analysis node_count, reference src/cly_mt.c:1352-1362) */
+__global__ __launch_bounds__(256) void k_taxon_count(const uint32_t *__restrict__ tid, const uint32_t *__restrict__ weight,
+						     uint64_t n, unsigned long long *__restrict__ counts)
+{
+	uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n)
+		atomicAdd(counts + tid[i], weight ? (unsigned long long)weight[i] : 1ull);
 }
 
 /* The merge-sort orders the classifier depends on, one array per lane:
@@ -323,6 +334,11 @@ extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
 	h.filter_min_length = ix->filter_min_length;
 	h.filter_min_score = ix->filter_min_score;
 	h.filter_min_score_LV3 = ix->filter_min_score_LV3;
+	if (ix->ref_tid && ix->p_tid) { /* taxonomy (per-read taxa in classB) */
+		if (upload(g, ix->ref_tid, ix->n_ref + 1, &h.ref_tid, err, errn)) return -1;
+		if (upload(g, ix->p_tid, ix->max_tid + 1, &h.p_tid, err, errn)) return -1;
+		h.max_tid = ix->max_tid;
+	}
 	const dsb_dindex_t *dptr;
 	if (upload(g, &h, 1, &dptr, err, errn)) return -1;
 	g->d = (dsb_dindex_t *)dptr;
@@ -482,6 +498,7 @@ struct dsb_gpu_batch {
 	std::vector<uint32_t> len;
 	std::vector<uint64_t> seq_off;
 	dbuf seq, d_seq_off, d_len;
+	dbuf d_tid, d_w;             /* per-read taxon of the last run (classB), weights for the counts */
 	std::vector<dsb_read_out_t> ro;
 	std::vector<dsb_hit_out_t> hits;
 	std::vector<int32_t> carry; /* max_read_l each read's part B used (src/cly.c:2953) */
@@ -657,7 +674,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	b->hits.clear();
 	if (n == 0)
 		return 0;
-	if (g->scale.ensure(4 * n + 4, err, errn) || g->ro.ensure(sizeof(dsb_read_out_t) * n + 64, err, errn) ||
+	if (b->d_tid.ensure(4 * n + 4, err, errn) || g->scale.ensure(4 * n + 4, err, errn) ||
+	    g->ro.ensure(sizeof(dsb_read_out_t) * n + 64, err, errn) ||
 	    g->mrl.ensure(4 * n + 4, err, errn) || g->hit_off.ensure(4 * n + 4, err, errn) ||
 	    g->cnt.ensure(64, err, errn) || g->ws_off.ensure(8 * n + 8, err, errn))
 		return -1;
@@ -891,11 +909,13 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		if (stats_on == 1)
 			k_classB<true><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
 							 g->order.as<uint32_t>(), cn, g->mrl.as<int32_t>(), g->ro.as<dsb_read_out_t>(),
-							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(), g->stats.as<unsigned long long>());
+							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(),
+							 b->d_tid.as<uint32_t>() + cb, g->stats.as<unsigned long long>());
 		else
 			k_classB<false><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
 							 g->order.as<uint32_t>(), cn, g->mrl.as<int32_t>(), g->ro.as<dsb_read_out_t>(),
-							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(), g->stats.as<unsigned long long>());
+							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(),
+							 b->d_tid.as<uint32_t>() + cb, g->stats.as<unsigned long long>());
 		T.ms_classB += ev_ms(g);
 		HIP_OK(hipGetLastError());
 		double td = now_ms();
@@ -984,6 +1004,43 @@ extern "C" const dsb_hit_out_t *dsb_gpu_batch_hits(const dsb_gpu_batch *b) { ret
 extern "C" const int32_t *dsb_gpu_batch_carry(const dsb_gpu_batch *b) { return b->carry.data(); }
 extern "C" uint64_t dsb_gpu_batch_n(const dsb_gpu_batch *b) { return b->n; }
 extern "C" uint64_t dsb_gpu_batch_bases(const dsb_gpu_batch *b) { return b->tot; }
+
+extern "C" int dsb_gpu_batch_counts(dsb_index *ix, dsb_gpu_batch *b, const uint32_t *weights, uint64_t *dev_counts,
+				    uint64_t n_counts, char *err, size_t errn)
+{
+	dsb_gpu_dev *g = (dsb_gpu_dev *)ix->gpu;
+	pthread_mutex_lock(&g->mu);
+	int rc = -1;
+	do {
+		if (hipSetDevice(g->device) != hipSuccess || !g->h.p_tid || n_counts < ix->max_tid + 1) {
+			snprintf(err, errn, "taxon counts: no taxonomy on the device or a table of %lu < max_tid + 1",
+				 (unsigned long)n_counts);
+			break;
+		}
+		if (!b->d_tid.p) {
+			snprintf(err, errn, "taxon counts before any run of the batch");
+			break;
+		}
+		hipStream_t s = g->stream;
+		if (hipMemsetAsync(dev_counts, 0, 8 * n_counts, s) != hipSuccess)
+			break;
+		if (weights) {
+			if (b->d_w.ensure(4 * b->n + 4, err, errn) ||
+			    hipMemcpyAsync(b->d_w.p, weights, 4 * b->n, hipMemcpyHostToDevice, s) != hipSuccess)
+				break;
+		}
+		if (b->n)
+			k_taxon_count<<<(uint32_t)((b->n + 255) / 256), 256, 0, s>>>(b->d_tid.as<uint32_t>(),
+				weights ? b->d_w.as<uint32_t>() : nullptr, b->n, (unsigned long long *)dev_counts);
+		if (hipGetLastError() != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+			snprintf(err, errn, "taxon counts: kernel failed");
+			break;
+		}
+		rc = 0;
+	} while (0);
+	pthread_mutex_unlock(&g->mu);
+	return rc;
+}
 
 extern "C" void dsb_gpu_batch_free(dsb_index *ix, dsb_gpu_batch *b)
 {

@@ -372,4 +372,5 @@ void dsb_index_host_view(const dsb_index *ix, dsb_dindex_t *d)
 	d->filter_min_length = ix->filter_min_length;
 	d->filter_min_score = ix->filter_min_score;
 	d->filter_min_score_LV3 = ix->filter_min_score_LV3;
+	d->ref_tid = ix->ref_tid; d->p_tid = ix->p_tid; d->max_tid = ix->max_tid;
 }

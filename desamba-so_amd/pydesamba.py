@@ -74,6 +74,8 @@ def lib(path: str | None = None):
     L.dsb_batch_carry.restype = C.c_int
     L.dsb_batch_taxa.argtypes = [vp, vp, C.c_int, C.c_void_p, C.c_void_p]
     L.dsb_batch_taxa.restype = C.c_int
+    L.dsb_batch_taxon_counts.argtypes = [vp, vp, C.c_int, C.c_void_p, u64]
+    L.dsb_batch_taxon_counts.restype = C.c_int
     L.dsb_batch_reads.argtypes = [vp]
     L.dsb_batch_reads.restype = u64
     L.dsb_batch_bases.argtypes = [vp]
@@ -197,6 +199,16 @@ class Batch:
         w = np.zeros(self.n_reads, dtype=np.uint64)
         self.L.dsb_batch_taxa(self.ix.h, self.h, flag, tid.ctypes.data, w.ctypes.data)
         return tid, w
+
+    def taxon_counts(self, counts, flag: int = 0):
+        """Per-taxon weights of the last run into `counts` (a torch int64 tensor on this GPU of
+        >= max_tid + 1 entries), reduced on the device (dsb_batch_taxon_counts)."""
+        import torch
+        assert counts.is_cuda and counts.dtype == torch.int64 and counts.is_contiguous()
+        torch.cuda.current_stream().synchronize()  # the library works on its own stream
+        if self.L.dsb_batch_taxon_counts(self.ix.h, self.h, flag, counts.data_ptr(), counts.numel()) != 0:
+            raise RuntimeError("dsb_batch_taxon_counts failed")
+        return counts
 
     def close(self):
         if self.h:

@@ -44,6 +44,12 @@ int dsb_batch_carry(dsb_batch *b, int32_t *carry_out);
 /* Per-read taxon as meta_analysis assigns it (ana_get_tid, reference src/cly_mt.c:902-961):
  * tid_out[i] (0 = unclassified); weight_out[i] = 1 or the read length (flag & 1). */
 int dsb_batch_taxa(void *idx, dsb_batch *b, int flag, uint32_t *tid_out, uint64_t *weight_out);
+/* The same taxa reduced on the GPU: dev_counts[t] = the summed weights (1, or the read length
+ * when flag & 1) of the last run's reads assigned taxon t (meta_analysis node_count, reference
+ * src/cly_mt.c:1352-1362).  dev_counts: device memory of the index's GPU, n_counts >=
+ * dsb_max_tid(idx) + 1 u64 entries, overwritten; the per-read taxa are computed by the classify
+ * kernels, so nothing but the table crosses PCIe.  Returns 0, or -1 (message on stderr). */
+int dsb_batch_taxon_counts(void *idx, dsb_batch *b, int flag, uint64_t *dev_counts, uint64_t n_counts);
 uint64_t dsb_batch_reads(dsb_batch *b);
 uint64_t dsb_batch_bases(dsb_batch *b);
 void dsb_batch_free(void *idx, dsb_batch *b);

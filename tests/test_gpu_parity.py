@@ -154,6 +154,29 @@ def test_batch_taxa_match_meta_analysis_rule(gpu_index, fixture_index, pyd):
         b.close()
 
 
+@pytest.mark.parametrize("name", ["mixed", "ont"])
+def test_device_taxon_counts_equal_the_meta_analysis_rule(gpu_index, fixture_index, pyd, name):
+    """dsb_batch_taxon_counts (per-read taxa from the classB kernel, counted on the GPU) against
+    the reference rule applied to the hermetic reference's records, for weights 1 and the read
+    length (meta_analysis flag & 1)."""
+    import numpy as np
+    import torch
+    parent = read_parents(os.path.join(fixture_index, "nodes.dmp"))
+    n_tax = gpu_index.max_tid() + 1
+    b = gpu_index.batch(golden(name + ".fq"))
+    try:
+        b.run(max_read_l=0)
+        want_tid = [ana_get_tid(r, parent, gpu_index.max_tid()) for _, r in groups(golden(name + ".herm.sam"))]
+        tid, wl = b.taxa(1)
+        assert list(tid) == want_tid
+        for flag, w in ((0, None), (1, wl)):
+            want = np.bincount(np.array(want_tid, dtype=np.int64), weights=w, minlength=n_tax).astype(np.int64)
+            got = b.taxon_counts(torch.full((n_tax,), -7, dtype=torch.int64, device="cuda"), flag).cpu().numpy()
+            assert (got == want).all()
+    finally:
+        b.close()
+
+
 def test_dlopen_consumer_example(fixture_index, tmp_path):
     """examples/consumer.c (a reference-style dlopen consumer) against the hermetic goldens."""
     exe = tmp_path / "consumer"
