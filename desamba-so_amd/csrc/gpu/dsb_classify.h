@@ -1730,6 +1730,9 @@ DSB_HD void dsb_sort_anchors(dsb_read_ws *w)
 	dsb_wsync();
 }
 
+/* chain_insert_M3's DP on LDS copies of a segment of up to this many anchors (wave kernels) */
+#define DSB_M3_LDS 256
+static_assert(4 * DSB_M3_LDS <= DSB_SORT_LDS * 2 && 2 * DSB_M3_LDS <= DSB_SORT_LDS, "M3 LDS staging fits the sort arrays");
 template <bool WAVE>
 DSB_HDN void dsb_chain_insert_M3(dsb_read_ws *w)
 {
@@ -1741,13 +1744,141 @@ DSB_HDN void dsb_chain_insert_M3(dsb_read_ws *w)
 		uint32_t chr_ed = chr_st + 1;
 		uint32_t ref_ID = A[chr_st].ref_ID;
 		uint32_t direction = A[chr_st].direction;
-		for (; chr_ed < n && A[chr_ed].ref_ID == ref_ID && A[chr_ed].direction == direction &&
-		       A[chr_ed].ref_offset - A[chr_ed - 1].ref_offset < 2000;
-		     chr_ed++);
+		if (!WAVE || DSB_SEQ(w, 64)) {
+			for (; chr_ed < n && A[chr_ed].ref_ID == ref_ID && A[chr_ed].direction == direction &&
+			       A[chr_ed].ref_offset - A[chr_ed - 1].ref_offset < 2000;
+			     chr_ed++);
+		} else { /* the first anchor that ends the segment, 64 at a time (only the first 1025 matter) */
+			uint32_t lane = dsb_lane();
+			uint32_t kb = chr_st + 1;
+			for (; kb < n && kb <= chr_st + 1024; kb += DSB_WV) {
+				uint32_t k = kb + lane;
+				int fail = k < n && !(A[k].ref_ID == ref_ID && A[k].direction == direction &&
+						      A[k].ref_offset - A[k - 1].ref_offset < 2000);
+				uint64_t bm = dsb_wballot(fail);
+				if (bm) {
+					kb += (uint32_t)__builtin_ctzll(bm);
+					break;
+				}
+			}
+			chr_ed = DSB_MIN(kb, n);
+		}
 		if (chr_ed - chr_st > 1024)
 			chr_ed = chr_st + 1024;
 		int32_t max_anchor = -1;
 		int max_score = 0, anchor_max_score;
+		uint32_t seg = chr_ed - chr_st;
+		if (WAVE && !DSB_SEQ(w, 64) && w->lds_key && seg <= DSB_M3_LDS) {
+			/* the segment's DP fields staged in LDS (the sort's key/id arrays are free again):
+			 * read offset, reference offset, mtch_len | score << 16, score_v, pre, flags */
+			uint32_t lane = dsb_lane();
+			uint32_t *Lq = (uint32_t *)w->lds_key, *Lt = Lq + DSB_M3_LDS, *Lms = Lt + DSB_M3_LDS;
+			int32_t *Lsv = (int32_t *)(Lms + DSB_M3_LDS);
+			int32_t *Lpre = (int32_t *)w->lds_id;
+			uint32_t *Lfl = (uint32_t *)w->lds_id + DSB_M3_LDS;
+			for (uint32_t k = lane; k < seg; k += DSB_WV) {
+				const dsb_anchor_t *a = A + chr_st + k;
+				Lq[k] = a->index_in_read;
+				Lt[k] = a->ref_offset;
+				Lms[k] = (uint32_t)a->mtch_len | ((uint32_t)(uint16_t)a->score << 16);
+				Lfl[k] = (uint32_t)(a->duplicate != 0) | ((uint32_t)(a->anchor_useless != 0) << 1);
+			}
+			dsb_wsync();
+			for (uint32_t ci = 0; ci < seg; ci++) {
+				uint32_t ms = Lms[ci];
+				uint32_t c_mtch = ms & 0xffffu;
+				anchor_max_score = (int)(int16_t)(ms >> 16);
+				int32_t c_pre = -1;
+				uint32_t max_t = Lt[ci] + 3;
+				uint32_t max_q = Lq[ci] + 3;
+				uint64_t best = 0;
+				for (int64_t pb = (int64_t)ci - 1; pb >= 0; pb -= DSB_WV) {
+					int64_t pi = pb - (int64_t)lane;
+					uint64_t cand = 0;
+					int brk = 0;
+					if (pi >= 0) {
+						uint32_t pq = Lq[pi], pt = Lt[pi], pm = Lms[pi] & 0xffffu;
+						if (!(pq + pm > max_q) && !(pt + pm > max_t)) {
+							if (pq + 1000 < max_q || pt + 1000 < max_t)
+								brk = 1;
+							else {
+								int indel = (int)(pq - pt - (max_q - max_t));
+								int ABS_indel = DSB_ABS(indel);
+								if (ABS_indel <= 200) {
+									int new_score = (int)((uint32_t)(Lsv[pi] + (int)c_mtch - (ABS_indel >> 4)) -
+											      ((max_q - pq) >> 8));
+									cand = ((uint64_t)((uint32_t)new_score ^ 0x80000000u) << 32) | (uint32_t)(pi + 1);
+								}
+							}
+						}
+					}
+					uint64_t bm = dsb_wballot(brk);
+					if (bm && lane >= (uint32_t)__builtin_ctzll(bm))
+						cand = 0;
+					best = DSB_MAX(best, cand);
+					if (bm)
+						break;
+				}
+				best = dsb_wmax64(best);
+				if (best) {
+					int bs = (int)((uint32_t)(best >> 32) ^ 0x80000000u);
+					if (bs > anchor_max_score) {
+						anchor_max_score = bs;
+						c_pre = (int32_t)((uint32_t)best - 1);
+					}
+				}
+				if (lane == 0) {
+					Lsv[ci] = anchor_max_score;
+					Lpre[ci] = c_pre;
+				}
+				dsb_wsync();
+				if (max_score < anchor_max_score) {
+					max_score = anchor_max_score;
+					max_anchor = (int32_t)ci;
+				}
+			}
+			for (uint32_t k = lane; k < seg; k += DSB_WV)
+				A[chr_st + k].pre = Lpre[k] < 0 ? -1 : (int32_t)chr_st + Lpre[k];
+			if (max_anchor < 0) { /* NULL dereference in the reference (all scores <= 0): unreachable */
+				dsb_wsync();
+				w->overflow |= 8;
+				return;
+			}
+			int sum_INDEL = 0, anchor_number = 1;
+			int32_t pre = max_anchor;
+			uint32_t fl = Lfl[max_anchor];
+			int sum_score = (fl & 1) ? 1 : (int)(int16_t)(Lms[max_anchor] >> 16);
+			int with_top = !(fl & 2);
+			for (; Lpre[pre] != -1; anchor_number++) {
+				int32_t pre_ = Lpre[pre];
+				sum_INDEL += (int)((Lq[pre] - Lq[pre_]) - (Lt[pre] - Lt[pre_]));
+				fl = Lfl[pre];
+				with_top |= !(fl & 2);
+				sum_score += (fl & 1) ? 1 : (int)(int16_t)(Lms[pre] >> 16);
+				pre = pre_;
+			}
+			uint32_t m_q = Lq[max_anchor], m_t = Lt[max_anchor], m_m = Lms[max_anchor] & 0xffffu;
+			uint32_t p_q = Lq[pre], p_t = Lt[pre];
+			dsb_wsync();
+			dsb_chain_t *nc = dsb_push_chain(w);
+			if (!nc)
+				return;
+			nc->chain_id = w->n_hit - 1;
+			nc->ref_ID = ref_ID;
+			nc->direction = (uint8_t)direction;
+			nc->q_t_dis = (int32_t)(m_t - m_q);
+			nc->t_st = p_t;
+			nc->t_ed = m_t + m_m;
+			nc->q_st = p_q;
+			nc->q_ed = m_q + m_m;
+			nc->with_top_anchor = (uint8_t)with_top;
+			nc->anchor_number = anchor_number;
+			nc->sum_score = sum_score;
+			nc->indel = sum_INDEL;
+			nc->cur = (int32_t)chr_st + max_anchor;
+			chr_st = chr_ed;
+			continue;
+		}
 		for (uint32_t ca = chr_st; ca < chr_ed; ca++) {
 			dsb_anchor_t *c_a = A + ca;
 			c_a->pre = -1;
