@@ -254,7 +254,7 @@ def main():
         for ph, c in ts["stats_phase"].items():
             b = phase_bytes(c) + (batch.n_bases if ph in ("fast0", "slow0") else 0)
             # the scoring kernel runs twice per chunk when part A is split (slow reads / the rest)
-            nl = (tms[0].get("n_launch_dela") or launches) if ph == "delA" else launches
+            nl = (tms[0].get("n_launch_dela") or launches) if ph == "delA" else (tms[0].get("n_launch_phase") or launches)
             ms = phase_ms[ph] / nl
             per_phase[ph] = {"algorithmic_bytes_per_launch": int(b / nl), "avg_launch_ms": round(ms, 3),
                              "launches_per_step": nl,

@@ -139,6 +139,7 @@ int dsb_classify_text(void *idx, const char *text, uint64_t text_n, int format, 
 		timing->n_chunks = gt.n_chunks;
 		timing->seed_positions = gt.seed_positions;
 		timing->n_launch_dela = gt.n_launch_dela;
+		timing->n_launch_phase = (int)gt.n_launch_phase;
 		for (int k = 0; k < DSB_N_STATS; k++) timing->stats[k] = gt.stats[k];
 	}
 	free(ro);
@@ -214,6 +215,7 @@ static void copy_timing(dsb_timing_t *t, const dsb_gpu_timing *gt)
 	t->n_chunks = gt->n_chunks;
 	t->seed_positions = gt->seed_positions;
 	t->n_launch_dela = gt->n_launch_dela;
+	t->n_launch_phase = (int)gt->n_launch_phase;
 	for (int k = 0; k < DSB_N_STATS; k++) t->stats[k] = gt->stats[k];
 }
 

@@ -142,6 +142,9 @@ enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, 
        DSB_ST_T_FILL,   /* stack-pattern fills of the windows */
        DSB_ST_PASS2,    /* seeding: seeds run again in the state machine's second pass */
        DSB_ST_REPLAY,   /* seeding: seeds replayed serially by the whole wave (both passes overflowed) */
+       DSB_ST_T_MPROBE, /* sdp_match: window probe k-mers + list heads */
+       DSB_ST_T_MWALK,  /* sdp_match: list walks + MEM_search extensions */
+       DSB_ST_T_COMB,   /* sdp_right / sdp_left: combine_chain */
        DSB_ST_N };
 /* wave clocks of a code region (timer kernels only: lane 0 accumulates into LDS, so that the
  * timing run pays no private-memory traffic for its counters) */
@@ -2528,9 +2531,12 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 					n_head = heads[n_kmer & KEY_MASK];
 				}
 			} else if (m <= n_i) {
+				uint64_t tp0 = DSB_T0();
 				kmer = probe(m, c_t_str);
 				head = heads[kmer & KEY_MASK];
+				DSB_T1(DSB_ST_T_MPROBE, tp0);
 			}
+			uint64_t tw0 = DSB_T0();
 			if (m <= n_i) {
 				if (w->stats) w->stats[DSB_ST_LOOKUP]++;
 				for (uint32_t he = head; he != DSB_HEMPTY; he = dsb_hstep(he, hnode, key_len)) {
@@ -2579,6 +2585,7 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 					}
 				}
 			}
+			DSB_T1(DSB_ST_T_MWALK, tw0);
 			uint32_t tot, off = dsb_wscan(cnt, &tot);
 			if (tot == 0)
 				continue;
@@ -2772,7 +2779,7 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 }
 
 /* combine_chain, src/cly.c:1758-1803 */
-DSB_HD int dsb_combine_chain(dsb_read_ws *w, int chain_ID, int dis, int isleft, int c_q_pos, int32_t *combined)
+DSB_HD int dsb_combine_chain_impl(dsb_read_ws *w, int chain_ID, int dis, int isleft, int c_q_pos, int32_t *combined)
 {
 	uint16_t key = (uint16_t)(dis & 0xff);
 	dsb_chain_t *c_h = w->hit + chain_ID;
@@ -2801,6 +2808,14 @@ DSB_HD int dsb_combine_chain(dsb_read_ws *w, int chain_ID, int dis, int isleft, 
 		key = sc[key].next;
 	}
 	return 0;
+}
+
+DSB_HD int dsb_combine_chain(dsb_read_ws *w, int chain_ID, int dis, int isleft, int c_q_pos, int32_t *combined)
+{
+	uint64_t t0 = DSB_T0();
+	int r = dsb_combine_chain_impl(w, chain_ID, dis, isleft, c_q_pos, combined);
+	DSB_T1(DSB_ST_T_COMB, t0);
+	return r;
 }
 
 /* sdp_right_M2, src/cly.c:2527-2672 */

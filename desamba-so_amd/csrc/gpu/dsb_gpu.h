@@ -32,6 +32,7 @@ typedef struct {
 	uint64_t n_reads, n_bases, n_retry, n_chunks;
 	uint64_t seed_positions; /* k-mer positions probed by the seed kernel (both strands) */
 	uint64_t n_launch_dela;  /* launches of the scoring kernel (2 per chunk when part A was split) */
+	uint64_t n_launch_phase; /* launches of each part-A phase kernel (1 per chunk, 2 when the halves are pipelined) */
 	uint64_t stats[DSB_N_STATS]; /* work counters DSB_ST_*: [32*ph, 32*ph+32) phase ph, [288,320) k_classB */
 } dsb_gpu_timing;
 

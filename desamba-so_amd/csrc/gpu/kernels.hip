@@ -238,6 +238,7 @@ struct dsb_gpu_dev {
 	hipStream_t stream;
 	hipStream_t stream2;     /* scoring of the reads that skip slow seeding, beside the slow phases */
 	hipEvent_t ev_a, ev_b, ev_fork, ev_r0, ev_r1;
+	hipEvent_t pev[2][DSB_PH_N + 1][2]; /* pipelined halves: k_seed and each phase launch, start / end */
 	pthread_mutex_t mu;
 	dsb_dindex_t h;          /* host copy holding device pointers */
 	dsb_dindex_t *d;         /* device copy */
@@ -300,6 +301,10 @@ extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
 	HIP_OK(hipEventCreate(&g->ev_fork));
 	HIP_OK(hipEventCreate(&g->ev_r0));
 	HIP_OK(hipEventCreate(&g->ev_r1));
+	for (int k = 0; k < 2; k++)
+		for (int ph = 0; ph <= DSB_PH_N; ph++)
+			for (int e = 0; e < 2; e++)
+				HIP_OK(hipEventCreate(&g->pev[k][ph][e]));
 	dsb_dindex_t &h = g->h;
 	memset(&h, 0, sizeof(h));
 	/* occ lines (128 B per 256 BWT symbols, re-laid out by the loader) + one zero line */
@@ -596,6 +601,22 @@ static int split_seed(void)
 	return v;
 }
 
+/* Pipelined halves (DSB_PIPE=1; off by default): the chunk's reads are split in two halves
+ * (longest first), each runs k_seed and every phase of part A in order on a stream of its own,
+ * B's k_seed starting when A's ends, so that B's bandwidth-bound k_seed runs beside A's
+ * latency-bound phases and each phase kernel's tail is filled by the other half.  Measured r02
+ * (C1, one box): 596.5k vs 591.4k reads/s, within box-to-box spread — every phase kernel already
+ * fills the wave slots, so co-running kernels trade slots rather than add throughput — and the
+ * per-kernel launch times then overlap, so the roofline's launch durations stay with the
+ * phase-by-phase order. */
+static int pipe_halves(void)
+{
+	static int v = -1;
+	if (v < 0)
+		v = getenv("DSB_PIPE") ? 1 : 0;
+	return v;
+}
+
 /* The split of part A (run_split) is off by default: with the slow reads' seeds no longer
  * replayed serially, the slow phases take ~9 ms in a row, while beside the scoring grid their
  * workgroups wait for its waves to free CUs (measured r02: 564k vs 555k reads/s).  DSB_SPLIT=1
@@ -744,6 +765,55 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			HIP_OK(hipMemcpyAsync(g->woA.p, woA.data(), 8 * woA.size(), hipMemcpyHostToDevice, s));
 			HIP_OK(hipMemcpyAsync(g->woB.p, woB.data(), 8 * woB.size(), hipMemcpyHostToDevice, s));
 			const uint32_t *oA = g->order.as<uint32_t>(), *oB = oA + h;
+			if (pipe_halves()) {
+				/* half A (longest reads) on the library stream, half B on the low-priority second
+				 * stream; phase launches interleaved so that both queues hold work early */
+				HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
+				hipEventRecord(g->ev_fork, s);
+				HIP_OK(hipStreamWaitEvent(g->stream2, g->ev_fork, 0));
+				hipStream_t hs[2] = {s, g->stream2};
+				const uint32_t *ho[2] = {oA, oB};
+				uint32_t hm[2] = {h, cn - h};
+				uint64_t htw[2] = {twA, twB};
+				const uint64_t *hwo[2] = {g->woA.as<uint64_t>(), g->woB.as<uint64_t>()};
+				for (int k = 0; k < 2; k++) {
+					/* B's k_seed starts when A's has finished: it then streams beside A's
+					 * latency-bound phases instead of sharing HBM with A's k_seed */
+					if (k == 1)
+						HIP_OK(hipStreamWaitEvent(hs[1], g->pev[0][0][1], 0));
+					hipEventRecord(g->pev[k][0][0], hs[k]);
+					if (htw[k])
+						k_seed<<<(uint32_t)((htw[k] * 64 + 255) / 256), 256, 0, hs[k]>>>(
+							g->d, cl, g->ws_off.as<uint64_t>(), wsb, hwo[k], ho[k], hm[k], htw[k]);
+					hipEventRecord(g->pev[k][0][1], hs[k]);
+				}
+				for (int ph = 0; ph < DSB_PH_N; ph++)
+					for (int k = 0; k < 2; k++) {
+						hipEventRecord(g->pev[k][ph + 1][0], hs[k]);
+						launch_phase(g, ph, stats_on, cl, wsb, ho[k], hm[k], hs[k]);
+						hipEventRecord(g->pev[k][ph + 1][1], hs[k]);
+					}
+				HIP_OK(hipGetLastError());
+				hipEventRecord(g->ev_r1, g->stream2);
+				HIP_OK(hipStreamWaitEvent(s, g->ev_r1, 0));
+				hipEventRecord(g->ev_b, s);
+				HIP_OK(hipEventSynchronize(g->ev_b));
+				/* wall accounting: k_seed of half A, then everything up to the join; per-phase
+				 * times are the sums of both halves' (overlapping) launch durations */
+				float f = 0;
+				hipEventElapsedTime(&f, g->pev[0][0][0], g->pev[0][0][1]);
+				T.ms_seed += f;
+				hipEventElapsedTime(&f, g->pev[0][0][1], g->ev_b);
+				T.ms_classA += f;
+				for (int ph = 0; ph < DSB_PH_N; ph++)
+					for (int k = 0; k < 2; k++) {
+						hipEventElapsedTime(&f, g->pev[k][ph + 1][0], g->pev[k][ph + 1][1]);
+						T.ms_phase[ph] += f;
+					}
+				T.n_launch_dela += 2;
+				T.n_launch_phase += 2;
+				ph0 = DSB_PH_N;
+			} else {
 			hipEventRecord(g->ev_a, s);
 			if (twA)
 				k_seed<<<(uint32_t)((twA * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
@@ -772,9 +842,12 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			(void)ms_ia;
 			HIP_OK(hipGetLastError());
 			ph0 = DSB_PH_ISLAND + 1;
+			T.n_launch_phase += 1;
+			}
 		} else {
 			tw = seed_words(len, cb, nullptr, cn, l_ek, word_off, &T.seed_positions);
 			HIP_OK(hipMemcpyAsync(g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
+			T.n_launch_phase += 1;
 		}
 		if (tw) {
 			hipEventRecord(g->ev_a, s);
@@ -783,7 +856,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			T.ms_seed += ev_ms(g);
 			HIP_OK(hipGetLastError());
 		}
-		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
+		if (ph0 < DSB_PH_N)
+			HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
 		/* island, fast seeding, resolve: every read */
 		for (int ph = ph0; ph < DSB_PH_N; ph++) {
 			hipEventRecord(g->ev_a, s);

@@ -16,12 +16,12 @@ FMT_SAM, FMT_SAM_FULL, FMT_DES, FMT_DES_FULL = 1, 2, 3, 4
 PHASES = ["island", "fast0", "fast1", "resolve_f", "slow0", "resolve_s0", "slow1", "resolve_s1", "delA"]
 ST_NAMES = ["occ", "occ_nib", "mem_search", "sa", "uni", "ref_pos", "getref_b", "anchor", "chain", "ek1", "ek2",
             "hash_b", "lookup", "node", "t_mem", "t_map", "t_build", "t_match", "t_win", "t_all", "t_dpm", "t_dps",
-            "t_fill", "pass2", "replay"]
+            "t_fill", "pass2", "replay", "t_mprobe", "t_mwalk", "t_comb"]
 ST_STRIDE = 32
 
 
 class Timing(C.Structure):
-    _fields_ = [("stats_on", C.c_int), ("pad", C.c_int), ("ms_total", C.c_double), ("ms_h2d", C.c_double),
+    _fields_ = [("stats_on", C.c_int), ("n_launch_phase", C.c_int), ("ms_total", C.c_double), ("ms_h2d", C.c_double),
                 ("ms_d2h", C.c_double), ("ms_encode", C.c_double), ("ms_seed", C.c_double),
                 ("ms_classA", C.c_double), ("ms_classB", C.c_double), ("ms_phase", C.c_double * 12),
                 ("n_reads", C.c_uint64),
@@ -30,7 +30,7 @@ class Timing(C.Structure):
                 ("stats", C.c_uint64 * 320)]
 
     def as_dict(self):
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("stats", "pad", "ms_phase")}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("stats", "ms_phase")}
         d["ms_phase"] = {n: float(self.ms_phase[i]) for i, n in enumerate(PHASES)}
         d["stats_phase"] = {ph: {n: int(self.stats[ST_STRIDE * p + i]) for i, n in enumerate(ST_NAMES)}
                             for p, ph in enumerate(PHASES)}

@@ -12,7 +12,7 @@ extern "C" {
 
 typedef struct {
 	int stats_on;          /* in: 1 collect algorithmic-work counters, 2 wave clocks per code region (slower kernel variants) */
-	int pad;
+	int n_launch_phase;   /* out: launches of each part-A phase kernel (chunks x pipelined halves) */
 	double ms_total;       /* host wall time of the GPU classify call */
 	double ms_h2d, ms_d2h; /* read upload / result download (host-measured) */
 	double ms_encode, ms_seed, ms_classA, ms_classB; /* per-kernel HIP-event times */
