@@ -145,6 +145,10 @@ enum { DSB_ST_OCC = 0, DSB_ST_OCC_NIB, DSB_ST_MEMSEARCH, DSB_ST_SA, DSB_ST_UNI, 
        DSB_ST_T_MPROBE, /* sdp_match: window probe k-mers + list heads */
        DSB_ST_T_MWALK,  /* sdp_match: list walks + MEM_search extensions */
        DSB_ST_T_COMB,   /* sdp_right / sdp_left: combine_chain */
+       DSB_ST_NWIN,     /* sdp_match calls (reference windows matched) */
+       DSB_ST_NBATCH,   /* sdp_match: 64-probe batches */
+       DSB_ST_NCAND,    /* sdp_match: list entries whose 9-mer and read range match (extended) */
+       DSB_ST_NSMS,     /* sdp_right / sdp_left: sparse-DP nodes processed */
        DSB_ST_N };
 /* wave clocks of a code region (timer kernels only: lane 0 accumulates into LDS, so that the
  * timing run pays no private-memory traffic for its counters) */
@@ -2513,8 +2517,10 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			n_kmer = probe((int)lane + 1, n_cts);
 			n_head = heads[n_kmer & KEY_MASK];
 		}
+		if (w->stats && lane == 0) w->stats[DSB_ST_NWIN]++;
 		for (int mb = 0; mb < n_i; mb += DSB_WV) {
 			int m = mb + (int)lane + 1;
+			if (w->stats && lane == 0) w->stats[DSB_ST_NBATCH]++;
 			uint32_t cnt = 0;
 			dsb_spd_t e0 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
 			const uint8_t *c_t_str = t_str;
@@ -2546,6 +2552,7 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 					uint32_t q_pos = dsb_hpos(he, key_len);
 					if (!(q_pos >= q_bg && q_pos <= q_ed))
 						continue;
+					if (w->stats) w->stats[DSB_ST_NCAND]++;
 					dsb_spd_t e;
 					int ok = 0;
 					if (isForward) {
@@ -2660,11 +2667,32 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 	if (c_a_i < 0)
 		return score - 10000;
 	uint64_t t_offset = dsb_gld(ix->ref_seq_offset + w->anc[c_a_i].ref_ID);
+	/* the anchor list is walked one pair ahead: the fields of the next pair's predecessor are
+	 * loaded at the top of each window, so that their round trip overlaps the window's work
+	 * instead of starting the next window (anchors are read-only in this phase) */
+	struct mid_anchor { uint32_t ref_offset, index_in_read, mtch_len; int32_t pre; };
+	auto ld_anchor = [&](int32_t i) -> mid_anchor {
+		const dsb_anchor_t *a = w->anc + i;
+		mid_anchor m;
+		m.ref_offset = dsb_gld(&a->ref_offset);
+		m.index_in_read = dsb_gld(&a->index_in_read);
+		m.pre = dsb_gld(&a->pre);
+		m.mtch_len = dsb_gld((const uint32_t *)&a->mtch_len) & 0xffffu; /* u16 mtch_len | i16 score */
+		return m;
+	};
+	mid_anchor ca = ld_anchor(c_a_i), pa;
+	pa.pre = -1;
+	if (ca.pre >= 0)
+		pa = ld_anchor(ca.pre);
 	while (c_a_i >= 0) {
-		dsb_anchor_t *c_a = w->anc + c_a_i;
+		const mid_anchor *c_a = &ca;
 		int32_t pre_i = c_a->pre;
 		if (pre_i >= 0) {
-			dsb_anchor_t *pre_a = w->anc + pre_i;
+			const mid_anchor *pre_a = &pa;
+			mid_anchor na;
+			na.pre = -1;
+			if (pa.pre >= 0)
+				na = ld_anchor(pa.pre);
 			int pre_mch = pre_a->mtch_len;
 			int pre_refoffset = (int)(pre_a->ref_offset - 3);
 			int total_ref_len = (int)(c_a->ref_offset - (uint32_t)(pre_refoffset + pre_mch) + 3);
@@ -2771,6 +2799,8 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 				}
 			}
 			DSB_T1(DSB_ST_T_DPM, tdp0);
+			ca = pa;
+			pa = na;
 		} else
 			score += c_a->mtch_len - DSB_S_A_KMER_L + 1;
 		c_a_i = pre_i;
@@ -2871,6 +2901,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 				break;
 		}
 		dsb_spd_t *c_sms = dsb_sms(w, current_sms++);
+		if (w->stats && dsb_lane() == 0) w->stats[DSB_ST_NSMS]++;
 		int max_score = (int)c_sms->len;
 		uint32_t max_pre_q = c_sms->q_pos + DSB_MAX_SMS_OVERLAP;
 		uint32_t max_pre_t = c_sms->t_pos + DSB_MAX_SMS_OVERLAP;
@@ -3022,6 +3053,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 				break;
 		}
 		dsb_spd_t *c_sms = dsb_sms(w, current_sms++);
+		if (w->stats && dsb_lane() == 0) w->stats[DSB_ST_NSMS]++;
 		int max_score = (int)c_sms->len;
 		uint32_t min_pre_q = c_sms->q_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
 		uint32_t min_pre_t = c_sms->t_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;

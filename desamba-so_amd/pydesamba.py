@@ -16,7 +16,7 @@ FMT_SAM, FMT_SAM_FULL, FMT_DES, FMT_DES_FULL = 1, 2, 3, 4
 PHASES = ["island", "fast0", "fast1", "resolve_f", "slow0", "resolve_s0", "slow1", "resolve_s1", "delA"]
 ST_NAMES = ["occ", "occ_nib", "mem_search", "sa", "uni", "ref_pos", "getref_b", "anchor", "chain", "ek1", "ek2",
             "hash_b", "lookup", "node", "t_mem", "t_map", "t_build", "t_match", "t_win", "t_all", "t_dpm", "t_dps",
-            "t_fill", "pass2", "replay", "t_mprobe", "t_mwalk", "t_comb"]
+            "t_fill", "pass2", "replay", "t_mprobe", "t_mwalk", "t_comb", "nwin", "nbatch", "ncand", "nsms"]
 ST_STRIDE = 32
 
 
