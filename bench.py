@@ -265,7 +265,9 @@ def main():
         if os.path.exists(tf):
             with open(tf) as f:
                 tj = json.load(f)
-            if tj.get("workload") == workload and tj.get("reads") == a.reads and tj.get("kernel") == KERNEL_OF[dom]:
+            # rocprof names carry the stats template argument ("k_wave_phase<8, 0>"): compare without it
+            tk = re.sub(r"<(\d+)(?:, \d+)*>", r"<\1>", tj.get("kernel") or "")
+            if tj.get("workload") == workload and tj.get("reads") == a.reads and tk == KERNEL_OF[dom]:
                 traffic = tj.get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 6), "traffic": traffic, "kernel": KERNEL_OF[dom],
