@@ -2902,6 +2902,12 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 		}
 		dsb_spd_t *c_sms = dsb_sms(w, current_sms++);
 		if (w->stats && dsb_lane() == 0) w->stats[DSB_ST_NSMS]++;
+		/* WAVE: the first batch of predecessors (one per lane) is loaded together with the node
+		 * itself, one round trip for both */
+		dsb_spd_t pre0 = {0, 0, 0, 0};
+		const int64_t pfirst = (int64_t)current_sms - 2;
+		if (WAVE && !DSB_SEQ(w, 4) && pfirst - (int64_t)dsb_lane() >= 0)
+			pre0 = *dsb_sms(w, pfirst - (int64_t)dsb_lane());
 		int max_score = (int)c_sms->len;
 		uint32_t max_pre_q = c_sms->q_pos + DSB_MAX_SMS_OVERLAP;
 		uint32_t max_pre_t = c_sms->t_pos + DSB_MAX_SMS_OVERLAP;
@@ -2932,7 +2938,8 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 				int64_t ps = pb - (int64_t)lane;
 				int cand = INT32_MIN, brk = 0;
 				if (ps >= 0) {
-					dsb_spd_t *c_pre = dsb_sms(w, ps);
+					const dsb_spd_t cp = (pb == pfirst) ? pre0 : *dsb_sms(w, ps);
+					const dsb_spd_t *c_pre = &cp;
 					int pre_q_ed = (int)(c_pre->q_pos + c_pre->len + DSB_S_A_KMER_L - 1);
 					int pre_t_ed = (int)(c_pre->t_pos + c_pre->len + DSB_S_A_KMER_L - 1);
 					if (!((uint32_t)pre_q_ed > max_pre_q) && !((uint32_t)pre_t_ed > max_pre_t)) {
@@ -3054,6 +3061,12 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 		}
 		dsb_spd_t *c_sms = dsb_sms(w, current_sms++);
 		if (w->stats && dsb_lane() == 0) w->stats[DSB_ST_NSMS]++;
+		/* WAVE: the first batch of predecessors (one per lane) is loaded together with the node
+		 * itself, one round trip for both */
+		dsb_spd_t pre0 = {0, 0, 0, 0};
+		const int64_t pfirst = (int64_t)current_sms - 2;
+		if (WAVE && !DSB_SEQ(w, 4) && pfirst - (int64_t)dsb_lane() >= 0)
+			pre0 = *dsb_sms(w, pfirst - (int64_t)dsb_lane());
 		int max_score = (int)c_sms->len;
 		uint32_t min_pre_q = c_sms->q_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
 		uint32_t min_pre_t = c_sms->t_pos + c_sms->len - DSB_MAX_SMS_OVERLAP + DSB_S_A_KMER_L - 1;
@@ -3082,7 +3095,8 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 				int64_t ps = pb - (int64_t)lane;
 				int cand = INT32_MIN, brk = 0;
 				if (ps >= 0) {
-					dsb_spd_t *c_pre = dsb_sms(w, ps);
+					const dsb_spd_t cp = (pb == pfirst) ? pre0 : *dsb_sms(w, ps);
+					const dsb_spd_t *c_pre = &cp;
 					if (!(c_pre->q_pos < min_pre_q) && !(c_pre->t_pos < min_pre_t)) {
 						if (min_pre_t + 600 < c_pre->t_pos)
 							brk = 1;
