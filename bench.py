@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Throughput of the MI355X classify path (BASELINE.json metric, config C1).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--index DIR]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--workload c1|c2|fixture]
+                  [--mix ont|c4] [--index DIR]
+
+--gpus N without a torch.distributed launcher starts N rank processes itself (one per GPU,
+before this process touches any GPU); under torchrun (WORLD_SIZE set) each rank is one process.
 
 A step = classify one batch of R synthetic ONT reads (lognormal, mean 8 kb, 5-15 % error)
 already resident in HBM (dsb_batch_run: seed + occ/rank + chaining + scoring on the GPU,
@@ -24,7 +28,13 @@ The JSON line carries:
                workload (profiles/), or null.
   cpu_baseline the reference classifier (oracle/_ref/deSAMBA, built from the reference
                sources by oracle/Makefile) on the host cores, on a bounded sample of the
-               same reads; rank 0 at N = 1 only.
+               same reads, at -t nproc (the value) and -t 1, plus the reference's own
+               read_classify(thread_num = nproc) through dlopen (oracle/_ref/abi_time); the
+               GPU's primary taxids for the sample are compared with the reference's records
+               (taxid_mismatch); rank 0 at N = 1 only.
+  dropin       the drop-in path end to end: one read_classify(idx, fastq, n, ...) call over
+               the whole batch (text in host memory -> SAM_FULL text in host memory: parse,
+               H2D, kernels, D2H, formatting), index preloaded; rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -69,13 +79,21 @@ def _tmp():
     return os.environ.get("TMPDIR", "/tmp")
 
 
-def unpack_index(rank: int) -> tuple[str, str]:
+# synthetic proxy indexes made by tools/make_proxy_index.sh with the reference's own builder
+WORKLOADS = {
+    "c1": ("C1-proxy-56Mbp", os.path.join(ROOT, "data", "c1_index.txz")),
+    "c2": ("C2-proxy-495Mbp-lek17", os.path.join(ROOT, "data", "c2_index.txz")),
+    "fixture": ("C0-fixture-1Mbp", os.path.join(ROOT, "tests", "golden", "fixture_index.txz")),
+}
+
+
+def unpack_index(rank: int, workload: str = "c1") -> tuple[str, str]:
     """-> (index dir, workload name).  Rank 0 unpacks, the others wait for it."""
-    txz = os.path.join(ROOT, "data", "c1_index.txz")
-    if os.path.exists(txz):
-        name, src = "C1-proxy-56Mbp", txz
-    else:
-        name, src = "C0-fixture-1Mbp", os.path.join(ROOT, "tests", "golden", "fixture_index.txz")
+    name, src = WORKLOADS[workload]
+    if not os.path.exists(src):
+        if workload != "c1":
+            raise SystemExit(f"{src} missing: build it with tools/make_proxy_index.sh {workload}")
+        name, src = WORKLOADS["fixture"]
     st = os.stat(src)
     key = hashlib.sha1(f"{src}:{st.st_size}:{int(st.st_mtime)}".encode()).hexdigest()[:12]
     d = os.path.join(_tmp(), f"dsb_index_{key}")
@@ -101,15 +119,18 @@ def unpack_index(rank: int) -> tuple[str, str]:
     return d, name
 
 
-def make_reads(index_dir: str, n: int, seed: int, mean_len: int) -> bytes:
-    """Synthetic ONT reads sampled from the index's own reference (tools/simulate.py)."""
-    path = os.path.join(_tmp(), f"dsb_reads_{os.path.basename(index_dir)}_{n}_{seed}_{mean_len}.fq")
+def make_reads(index_dir: str, n: int, seed: int, mean_len: int, mix: str = "ont") -> bytes:
+    """Synthetic reads sampled from the index's own reference (tools/simulate.py): ONT-like
+    (lognormal mean `mean_len`), or BASELINE C4's mix (150 bp + 20 kb ONT, 1:1, interleaved)."""
+    path = os.path.join(_tmp(), f"dsb_reads_{os.path.basename(index_dir)}_{n}_{seed}_{mean_len}_{mix}.fq")
     if not os.path.exists(path):
         import simulate
         t = time.time()
         genomes = simulate.read_fasta_genomes_from_index(index_dir)
         part = path + f".part{os.getpid()}"
-        simulate.write_fastq(simulate.simulate_reads(genomes, n, seed, "ont", mean_len), part)
+        gen = (simulate.simulate_c4_mix(genomes, n, seed) if mix == "c4"
+               else simulate.simulate_reads(genomes, n, seed, "ont", mean_len))
+        simulate.write_fastq(gen, part)
         os.rename(part, path)
         log(f"simulated {n} reads (seed {seed}) in {time.time() - t:.1f}s")
     with open(path, "rb") as f:
@@ -126,32 +147,159 @@ def fastq_head(fq: bytes, n: int) -> bytes:
 
 
 # ----------------------------------------------------------------------------- baseline
-def cpu_baseline(index_dir: str, fq: bytes, n_sample: int, threads: int):
-    """The reference CLI (oracle/_ref/deSAMBA, gcc -O3 build of the reference sources) on
-    the first n_sample reads; its own 'N sequences processed in T s' timer (starts after
-    the index load, reference src/cly_mt.c:527,557)."""
+def host_cpus() -> dict:
+    """nproc, the CPUs this process may run on, the cgroup CPU quota and the model name."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_quota": None,
+            "model": None}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            info["cgroup_quota"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return info
+
+
+def _ref_classify(index_dir: str, sample: bytes, threads: int, sam_out: str | None):
+    """The reference CLI on `sample`: (reads, seconds) from its own 'N sequences processed in
+    T s' timer (starts after the index load, reference src/cly_mt.c:527,557)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "deSAMBA")
-    if not os.path.exists(exe):
-        return None
-    sample = fastq_head(fq, n_sample)
-    nb = sum(len(l) for i, l in enumerate(sample.split(b"\n")) if i % 4 == 1)
     with tempfile.TemporaryDirectory(dir=_tmp()) as d:
         p = os.path.join(d, "sample.fq")
         with open(p, "wb") as f:
             f.write(sample)
-        t = time.time()
-        r = subprocess.run([exe, "classify", "-t", str(threads), "-o", os.path.join(d, "o.sam"), index_dir, p],
-                           capture_output=True, text=True, timeout=600)
-        wall = time.time() - t
+        r = subprocess.run([exe, "classify", "-t", str(threads), "-o", sam_out or os.path.join(d, "o.sam"),
+                            index_dir, p], capture_output=True, text=True, timeout=900)
     m = re.search(r"(\d+) sequences processed in ([0-9.]+)s", r.stdout + r.stderr)
     if r.returncode != 0 or not m:
         log("reference CPU run failed:", r.returncode, (r.stdout + r.stderr)[-400:])
         return None
-    n, secs = int(m.group(1)), float(m.group(2))
-    return {"value": round(n / secs, 1), "unit": "reads/s", "cores": threads, "kind": "reference",
-            "gbases_per_s": round(nb / secs / 1e9, 5),
-            "sample": f"first {n} reads ({nb / 1e6:.1f} Mbp) of rank 0's batch, `deSAMBA classify -t {threads}` "
-                      f"(gcc -O3 build of the reference sources), own timer {secs:.2f}s, wall {wall:.1f}s incl. index load"}
+    return int(m.group(1)), float(m.group(2))
+
+
+def _ref_dropin(index_dir: str, sample: bytes, threads: int):
+    """The reference's read_classify(thread_num) through dlopen (oracle/_ref/abi_time), index
+    preloaded by its load_index, one call over the sample held in memory."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "abi_time")
+    lib = os.path.join(ROOT, "oracle", "_ref", "libdesamba.so")
+    if not (os.path.exists(exe) and os.path.exists(lib)):
+        return None
+    with tempfile.TemporaryDirectory(dir=_tmp()) as d:
+        p = os.path.join(d, "sample.fq")
+        with open(p, "wb") as f:
+            f.write(sample)
+        r = subprocess.run([exe, lib, index_dir, p, str(threads)], capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        log("reference read_classify run failed:", r.returncode, r.stderr[-400:])
+        return None
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def n_bases(fq: bytes) -> int:
+    return sum(len(l) for i, l in enumerate(fq.split(b"\n")) if i % 4 == 1)
+
+
+def cpu_baseline(index_dir: str, fq: bytes, n_sample: int, n_sample_t1: int, gpu_sam_sample: bytes | None):
+    """The reference (oracle/_ref, gcc -O3 build of the reference sources) on this box's host
+    cores over the first reads of rank 0's batch: `deSAMBA classify -t nproc` (the value), the
+    same at -t 1 on a smaller sample, and read_classify(thread_num = nproc) through dlopen.
+    The -t nproc run's primary taxids are compared with the GPU's records for the same reads."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "deSAMBA")):
+        return None
+    cpus = host_cpus()
+    nproc = cpus["nproc"]
+    sample = fastq_head(fq, n_sample)
+    nb = n_bases(sample)
+    with tempfile.TemporaryDirectory(dir=_tmp()) as d:
+        sam = os.path.join(d, "o.sam")
+        t = time.time()
+        r = _ref_classify(index_dir, sample, nproc, sam)
+        wall = time.time() - t
+        if r is None:
+            return None
+        n, secs = r
+        mism = None
+        if gpu_sam_sample is not None:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            from samutil import compare
+            with open(sam, "rb") as f:
+                c = compare(f.read(), gpu_sam_sample)
+            mism = {"reads": c["reads"], "taxid_mismatch": c["taxid_mismatch"], "mapped_mismatch": c["mapped_mismatch"],
+                    "full_record_mismatch": c["full_mismatch"]}
+    out = {"value": round(n / secs, 1), "unit": "reads/s", "cores": nproc, "kind": "reference",
+           "gbases_per_s": round(nb / secs / 1e9, 5), "host": cpus,
+           "sample": f"first {n} reads ({nb / 1e6:.1f} Mbp) of rank 0's batch, `deSAMBA classify -t {nproc}` "
+                     f"(gcc -O3 build of the reference sources), own timer {secs:.2f}s, wall {wall:.1f}s incl. index load",
+           "taxid_check_vs_gpu": mism}
+    s1 = fastq_head(fq, n_sample_t1)
+    r1 = _ref_classify(index_dir, s1, 1, None)
+    if r1:
+        out["t1"] = {"value": round(r1[0] / r1[1], 1), "reads": r1[0], "secs": r1[1],
+                     "gbases_per_s": round(n_bases(s1) / r1[1] / 1e9, 5)}
+    dj = _ref_dropin(index_dir, sample, nproc)
+    if dj:
+        out["read_classify"] = {"value": round(n / dj["secs"], 1), "secs": dj["secs"], "thread_num": nproc,
+                                "reads": n, "output_bytes": dj["output_bytes"]}
+    return out
+
+
+def dropin_leg(idx, fq: bytes, n_reads: int, nb: int, batch_sam_full_sha: str | None):
+    """One read_classify call over the whole batch (reference desamba.h:23): FASTQ text in host
+    memory -> SAM_FULL text in host memory, the index preloaded; the output is checked against
+    the batch path's records for the same reads."""
+    import ctypes as C
+    L = idx.L
+    out, n = C.c_void_p(), C.c_uint64(0)
+    t = time.perf_counter()
+    L.read_classify(idx.h, fq, len(fq), C.byref(out), C.byref(n), 7, 1)
+    secs = time.perf_counter() - t
+    text = C.string_at(out.value, n.value) if out.value else b""
+    L.dsb_free(out)
+    same = None
+    if batch_sam_full_sha is not None:
+        same = hashlib.sha256(text).hexdigest() == batch_sam_full_sha
+    return {"value": round(n_reads / secs, 1), "unit": "reads/s", "secs": round(secs, 4),
+            "gbases_per_s": round(nb / secs / 1e9, 4), "reads": n_reads, "input_bytes": len(fq),
+            "output_bytes": n.value, "identical_to_batch_records": same,
+            "what": "read_classify(idx, fastq_text, n, &out, &out_n, 7, 1): parse + H2D + kernels + D2H + "
+                    "SAM_FULL formatting, index preloaded"}
+
+
+def spawn_ranks(n: int) -> int:
+    """--gpus N without a launcher: start N rank processes (RANK/LOCAL_RANK/WORLD_SIZE, rendezvous
+    on 127.0.0.1) before this process touches any GPU, forward their exit status.  Rank 0 prints
+    the JSON line."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                log(f"rank pid {p.pid} exited with {c}; stopping the other ranks")
+                for q in live:
+                    q.kill()
+        time.sleep(0.2)
+    return rc
 
 
 # ----------------------------------------------------------------------------- main
@@ -162,12 +310,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reads", type=int, default=100000, help="reads per rank")
     ap.add_argument("--mean-len", type=int, default=8000)
-    ap.add_argument("--index", default=None, help="index directory (default: C1 proxy)")
-    ap.add_argument("--cpu-sample", type=int, default=16000, help="reads in the CPU baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS), help="proxy index (data/<w>_index.txz)")
+    ap.add_argument("--mix", default="ont", choices=["ont", "c4"], help="ONT reads, or C4's 150 bp + 20 kb 1:1 mix")
+    ap.add_argument("--index", default=None, help="index directory (overrides --workload)")
+    ap.add_argument("--cpu-sample", type=int, default=16000, help="reads in the CPU baseline sample (-t nproc)")
+    ap.add_argument("--cpu-sample-t1", type=int, default=2000, help="reads in the -t 1 CPU sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the end-to-end read_classify leg")
     ap.add_argument("--no-stats", action="store_true", help="skip the work-counter run (roofline)")
     a = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -194,8 +348,10 @@ def main():
     if a.index:
         index_dir, workload = a.index, os.path.basename(os.path.normpath(a.index))
     else:
-        index_dir, workload = unpack_index(rank)
-    fq = make_reads(index_dir, a.reads, 1000 + rank, a.mean_len)
+        index_dir, workload = unpack_index(rank, a.workload)
+    if a.mix == "c4":
+        workload += "+C4-mix-150bp-20kb"
+    fq = make_reads(index_dir, a.reads, 1000 + rank, a.mean_len, a.mix)
     if dist:
         dist.barrier()
     t = time.time()
@@ -275,9 +431,16 @@ def main():
                 "launches_per_step": d["launches_per_step"], "avg_launch_ms": d["avg_launch_ms"], "phases": per_phase}
         stats = {"phases": ts["stats_phase"], "classB": ts["stats_B"]}
 
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(index_dir, fq, min(a.cpu_sample, batch.n_reads), a.cpu_threads)
+    cpu = dropin = None
+    if rank == 0 and world == 1:
+        import pydesamba as P
+        n_s = min(a.cpu_sample, batch.n_reads)
+        if not a.no_cpu:
+            cpu = cpu_baseline(index_dir, fq, n_s, min(a.cpu_sample_t1, batch.n_reads),
+                               batch.format_range(0, n_s, P.FMT_SAM))
+        if not a.no_dropin:
+            full_sha = hashlib.sha256(batch.format(P.FMT_SAM_FULL)).hexdigest()
+            dropin = dropin_leg(idx, fq, batch.n_reads, batch.n_bases, full_sha)
 
     if rank == 0:
         value = reads_total / elapsed
@@ -285,9 +448,11 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "reads/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic ONT reads (tools/simulate.py, lognormal mean 8 kb, 5-15% error) from a synthetic reference",
+            "data": ("synthetic ONT reads (tools/simulate.py, lognormal mean 8 kb, 5-15% error)" if a.mix == "ont" else
+                     "synthetic C4 mix (tools/simulate.py: 150 bp 1% error + ONT lognormal mean 20 kb, 1:1 interleaved)")
+                    + " from a synthetic reference",
             "config": {"workload": workload, "reads_per_rank": batch.n_reads, "mbases_per_rank": round(batch.n_bases / 1e6, 2),
-                       "mean_len": a.mean_len, "parallelism": f"reads sharded over {world} GPU(s), index replicated",
+                       "mean_len": round(batch.n_bases / max(1, batch.n_reads)), "read_mix": a.mix, "parallelism": f"reads sharded over {world} GPU(s), index replicated",
                        "taxon_reduce": f"all_reduce({dist.get_backend()})" if world > 1 else "none"},
             "gbases_per_s": round(bases_total / elapsed / 1e9, 4),
             "classified_reads": classified,
@@ -297,9 +462,14 @@ def main():
             "phase_ms_classA": {k: round(v, 2) for k, v in phase_ms.items()},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "dropin": dropin,
         }
         if cpu:
             line["vs_cpu_baseline"] = round(value / cpu["value"], 2)
+            if cpu.get("taxid_check_vs_gpu"):
+                line["taxid_mismatch"] = cpu["taxid_check_vs_gpu"]["taxid_mismatch"]
+            if dropin and cpu.get("read_classify"):
+                line["dropin_vs_reference_read_classify"] = round(dropin["value"] / cpu["read_classify"]["value"], 2)
         if stats:
             line["work_counters"] = stats
         print(json.dumps(line), flush=True)

@@ -19,7 +19,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <sys/mman.h>
 #include "dsb_host.h"
+#include "pipeline.h"
 #include "gpu/dsb_gpu.h"
 #include "../../include/desamba.h"
 #include "../../include/desamba_mi355x.h"
@@ -67,6 +69,7 @@ void load_index(void **idx, const char *dirPath)
 		dsb_index_free_host_tables(ix);
 	pthread_mutex_init(&ix->state_mutex, NULL);
 	ix->states = NULL;
+	ix->pool = dsb_pool_new(dsb_host_threads() - 1);
 	*idx = ix;
 }
 
@@ -92,62 +95,74 @@ static struct dsb_thread_state *thread_state(dsb_index *ix, int thread_id, int t
 	return s;
 }
 
+static void copy_gpu_timing(dsb_timing_t *t, const dsb_gpu_timing *gt)
+{
+	t->ms_h2d = gt->ms_h2d;
+	t->ms_d2h = gt->ms_d2h;
+	t->ms_encode = gt->ms_encode;
+	t->ms_seed = gt->ms_seed;
+	t->ms_classA = gt->ms_classA;
+	t->ms_classB = gt->ms_classB;
+	for (int k = 0; k < 12; k++) t->ms_phase[k] = gt->ms_phase[k];
+	t->n_reads = gt->n_reads;
+	t->n_bases = gt->n_bases;
+	t->n_retry = gt->n_retry;
+	t->n_chunks = gt->n_chunks;
+	t->seed_positions = gt->seed_positions;
+	t->n_launch_dela = gt->n_launch_dela;
+	t->n_launch_phase = (int)gt->n_launch_phase;
+	for (int k = 0; k < DSB_N_STATS; k++) t->stats[k] = gt->stats[k];
+}
+
+/* text (plain FASTQ/FASTA, resident for the call) -> records through the streaming pipeline */
+static int classify_resident(dsb_index *ix, const char *text, uint64_t text_n, int format, int *max_read_l,
+			     char **output, uint64_t *output_n, dsb_timing_t *timing)
+{
+	char err[1024];
+	dsb_pipe_timing pt;
+	int st = timing ? timing->stats_on : 0;
+	int rc = dsb_pipeline_classify(ix, (dsb_pool *)ix->pool, text, text_n, format, 5, max_read_l, st, output,
+				       output_n, &pt, err, sizeof(err));
+	if (rc) {
+		fprintf(stderr, "[read_classify] %s\n", err);
+		return -1;
+	}
+	if (timing) {
+		memset(timing, 0, sizeof(*timing));
+		timing->stats_on = st;
+		copy_gpu_timing(timing, &pt.gpu);
+		timing->ms_total = pt.ms_total;
+		timing->ms_parse = pt.ms_parse;
+		timing->ms_gather = pt.ms_gather;
+		timing->ms_format = pt.ms_format;
+		timing->ms_wait_gpu = pt.ms_wait_gpu;
+		timing->n_batches = pt.n_batches;
+		timing->n_devices = pt.n_devices;
+		timing->n_view_records = pt.n_view_records;
+		timing->n_copied_records = pt.n_copied_records;
+	}
+	return 0;
+}
+
 int dsb_classify_text(void *idx, const char *text, uint64_t text_n, int format, int *max_read_l, char **output,
 		      uint64_t *output_n, dsb_timing_t *timing)
 {
 	dsb_index *ix = idx;
-	char err[1024];
-	dsb_reads_t reads;
-	memset(&reads, 0, sizeof(reads));
-	dsb_parse_reads(text, text_n, &reads);
-	dsb_read_out_t *ro = calloc(reads.n + 1, sizeof(dsb_read_out_t));
-	dsb_hit_out_t *hits = NULL;
-	uint64_t n_hits = 0;
-	dsb_gpu_timing gt;
-	memset(&gt, 0, sizeof(gt));
-	if (dsb_gpu_classify(ix, &reads, max_read_l, ro, &hits, &n_hits, timing ? timing->stats_on : 0, &gt, err,
-			     sizeof(err))) {
-		fprintf(stderr, "[read_classify] %s\n", err);
-		free(ro);
-		free(hits);
-		dsb_reads_free(&reads);
+	char *buf = NULL;
+	uint64_t len = 0;
+	int owned = 0;
+	if (dsb_inflate_if_gzip(text, text_n, &buf, &len, &owned)) {
+		fprintf(stderr, "[dsb_classify_text] cannot decompress input\n");
 		return -1;
 	}
-	dsb_str out = {0, 0, 0};
-	for (uint64_t i = 0; i < reads.n; i++)
-		dsb_format_read(&out, ix, &reads, i, ro + i, hits + ro[i].hit_off, format, 5);
-	*output_n = out.l;
-	*output = malloc(out.l + 1);
-	memset(*output, 0, out.l + 1);
-	if (out.l) memcpy(*output, out.s, out.l);
-	free(out.s);
-	if (timing) {
-		int st = timing->stats_on;
-		memset(timing, 0, sizeof(*timing));
-		timing->stats_on = st;
-		timing->ms_total = gt.ms_total;
-		timing->ms_h2d = gt.ms_h2d;
-		timing->ms_d2h = gt.ms_d2h;
-		timing->ms_encode = gt.ms_encode;
-		timing->ms_seed = gt.ms_seed;
-		timing->ms_classA = gt.ms_classA;
-		timing->ms_classB = gt.ms_classB;
-		for (int k = 0; k < 12; k++) timing->ms_phase[k] = gt.ms_phase[k];
-		timing->n_reads = gt.n_reads;
-		timing->n_bases = gt.n_bases;
-		timing->n_retry = gt.n_retry;
-		timing->n_chunks = gt.n_chunks;
-		timing->seed_positions = gt.seed_positions;
-		timing->n_launch_dela = gt.n_launch_dela;
-		timing->n_launch_phase = (int)gt.n_launch_phase;
-		for (int k = 0; k < DSB_N_STATS; k++) timing->stats[k] = gt.stats[k];
-	}
-	free(ro);
-	free(hits);
-	dsb_reads_free(&reads);
-	return 0;
+	int rc = classify_resident(ix, buf, len, format, max_read_l, output, output_n, timing);
+	if (owned) free(buf);
+	return rc;
 }
 
+/* reference read_classify (cly_mt.c:1309-1316, read_classify_core :1041-1081): the input text is
+ * classified where it lies (a path is mapped, gzip is inflated), batch by batch over every GPU
+ * holding the index, and the SAM_FULL records come back in one malloc'd buffer */
 void read_classify(void *idx, char *input, uint64_t input_n, char **output, uint64_t *output_n, int thread_id,
 		   int thread_num)
 {
@@ -158,23 +173,26 @@ void read_classify(void *idx, char *input, uint64_t input_n, char **output, uint
 	dsb_index *ix = idx;
 	struct dsb_thread_state *st = thread_state(ix, thread_id, thread_num);
 	char *buf = NULL;
-	uint64_t len = 0;
+	uint64_t len = 0, unmap = 0;
 	int owned = 0;
 	if (input_n == (uint64_t)-1) {
-		if (dsb_slurp_path(input, &buf, &len)) {
+		if (dsb_open_path(input, &buf, &len, &unmap)) {
 			char msg[4200];
 			snprintf(msg, sizeof(msg), "fail to open file '%s' : No such file or directory", input);
 			fatal("read_classify", msg);
 		}
-		owned = 1;
+		owned = unmap == 0;
 	} else if (dsb_inflate_if_gzip(input, input_n, &buf, &len, &owned)) {
 		fatal("read_classify", "cannot decompress input");
 	}
 	int mrl = st->max_read_l;
-	if (dsb_classify_text(ix, buf, len, DSB_OUT_SAM_FULL, &mrl, output, output_n, NULL))
+	if (classify_resident(ix, buf, len, DSB_OUT_SAM_FULL, &mrl, output, output_n, NULL))
 		fatal("read_classify", "GPU classify failed");
 	st->max_read_l = mrl;
-	if (owned) free(buf);
+	if (unmap)
+		munmap(buf, unmap);
+	else if (owned)
+		free(buf);
 }
 
 void meta_analysis(void *idx, char *input, uint64_t input_n, char **output, uint64_t *output_n, int thread_id,
@@ -223,7 +241,12 @@ dsb_batch *dsb_batch_create(void *idx, const char *text, uint64_t text_n, dsb_ti
 {
 	char err[1024];
 	dsb_batch *b = calloc(1, sizeof(*b));
-	dsb_parse_reads(text, text_n, &b->reads);
+	/* the batch outlives the caller's text: its records view a copy */
+	char *own = malloc(text_n + 1);
+	if (text_n) memcpy(own, text, text_n);
+	own[text_n] = 0;
+	dsb_parse_reads(own, text_n, &b->reads);
+	b->reads.text_owner = own;
 	dsb_gpu_timing gt;
 	memset(&gt, 0, sizeof(gt));
 	if (dsb_gpu_batch_upload(idx, &b->reads, &b->g, &gt, err, sizeof(err))) {
@@ -276,7 +299,7 @@ int dsb_batch_taxa(void *idx, dsb_batch *b, int flag, uint32_t *tid_out, uint64_
 	for (uint64_t i = 0; i < b->reads.n; i++) {
 		const dsb_rec_t *rec = b->reads.rec + i;
 		/* the SAM text meta_analysis parses prints SEQ with %s: its length is strlen */
-		weight_out[i] = (flag & 1) ? (uint64_t)strlen(b->reads.arena + rec->seq_off) : 1;
+		weight_out[i] = (flag & 1) ? dsb_cstr_len(rec->seq, rec->seq_l) : 1;
 		tid_out[i] = dsb_read_taxon(hits + ro[i].hit_off, ro[i].n_hit, ix->ref_tid, ix->p_tid, ix->max_tid);
 	}
 	return 0;
@@ -292,7 +315,7 @@ int dsb_batch_taxon_counts(void *idx, dsb_batch *b, int flag, uint64_t *dev_coun
 	if (flag & 1) { /* strlen of each SEQ, as meta_analysis' parse of the SAM text sees it */
 		w = malloc(sizeof(uint32_t) * (b->reads.n + 1));
 		for (uint64_t i = 0; i < b->reads.n; i++)
-			w[i] = (uint32_t)strlen(b->reads.arena + b->reads.rec[i].seq_off);
+			w[i] = (uint32_t)dsb_cstr_len(b->reads.rec[i].seq, b->reads.rec[i].seq_l);
 	}
 	int rc = dsb_gpu_batch_counts(ix, b->g, w, dev_counts, n_counts, err, sizeof(err));
 	free(w);
@@ -312,6 +335,14 @@ int dsb_batch_carry(dsb_batch *b, int32_t *carry_out)
 uint64_t dsb_batch_reads(dsb_batch *b) { return b->reads.n; }
 uint64_t dsb_batch_bases(dsb_batch *b) { return dsb_gpu_batch_bases(b->g); }
 uint64_t dsb_max_tid(void *idx) { return ((dsb_index *)idx)->max_tid; }
+int dsb_index_devices(void *idx, int *device_ids, int max_ids)
+{
+	dsb_index *ix = idx;
+	int n = dsb_gpu_n_devices(ix);
+	for (int k = 0; k < n && k < max_ids; k++)
+		device_ids[k] = dsb_gpu_device_id(ix, k);
+	return n;
+}
 
 void dsb_batch_free(void *idx, dsb_batch *b)
 {
@@ -322,6 +353,45 @@ void dsb_batch_free(void *idx, dsb_batch *b)
 }
 
 /* ------------------------------------------------------------------ extensions */
+/* The records the parser yields for `text` (kseq + kt_pipeline semantics), one line each:
+ * name, seq, qual (or "(null)") as printf("%s") prints them, '\t'-separated; slow != 0 turns
+ * the zero-copy FASTQ fast path off, batch_reads > 0 parses in batches of that many reads
+ * (the streaming parser).  Host only: lets the CPU tests pin the parser. */
+int dsb_parse_dump(const char *text, uint64_t text_n, int slow, uint64_t batch_reads, char **output,
+		   uint64_t *output_n)
+{
+	if (slow)
+		setenv("DSB_PARSE_SLOW", "1", 1);
+	dsb_parser *p = dsb_parser_new(text, text_n);
+	if (slow)
+		unsetenv("DSB_PARSE_SLOW");
+	dsb_reads_t r;
+	memset(&r, 0, sizeof(r));
+	dsb_str out = {0, 0, 0};
+	for (;;) {
+		r.n = 0;
+		if (!dsb_parser_next(p, &r, batch_reads ? batch_reads : UINT64_MAX, UINT64_MAX))
+			break;
+		for (uint64_t i = 0; i < r.n; i++) {
+			const dsb_rec_t *c = r.rec + i;
+			dsb_str_put(&out, c->name, dsb_cstr_len(c->name, c->name_l));
+			dsb_str_printf(&out, "\t%u\t", c->seq_l);
+			dsb_str_put(&out, c->seq, dsb_cstr_len(c->seq, c->seq_l));
+			dsb_str_put(&out, "\t", 1);
+			if (c->qual)
+				dsb_str_put(&out, c->qual, dsb_cstr_len(c->qual, c->qual_l));
+			else
+				dsb_str_put(&out, "(null)", 6);
+			dsb_str_put(&out, "\n", 1);
+		}
+	}
+	free(r.rec);
+	dsb_parser_free(p);
+	*output_n = out.l;
+	*output = out.s ? out.s : calloc(1, 1);
+	return 0;
+}
+
 const char *dsb_version(void)
 {
 	return "desamba-mi355x 0.1 (gfx950)";
@@ -342,6 +412,7 @@ void dsb_unload_index(void *idx)
 	dsb_index *ix = idx;
 	if (!ix) return;
 	dsb_gpu_free(ix);
+	dsb_pool_free((dsb_pool *)ix->pool);
 	dsb_index_free_host_tables(ix);
 	free(ix->Q_MEM); free(ix->ref_name); free(ix->ref_tid); free(ix->p_tid); free(ix->ref_seq_l); free(ix->ref_seq_offset); free(ix->tax);
 	struct dsb_thread_state *s = ix->states;

@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <pthread.h>
+#include <string.h>
 #include "dsb_types.h"
 
 #ifdef __cplusplus
@@ -18,6 +19,7 @@ extern "C" {
 #endif
 
 /* ------------------------------------------------------------------ index */
+#define DSB_MAX_GPUS 16
 typedef struct {
 	uint32_t p_tid;
 	char rank[20];
@@ -48,8 +50,11 @@ typedef struct dsb_index {
 	int filter_min_length, filter_min_score, filter_min_score_LV3;
 	/* taxonomy (cly_mt.c:590-670) */
 	dsb_taxon_t *tax; uint64_t max_tid;
-	/* device side (dsb_gpu.c) */
+	/* device side (gpu/kernels.hip): the index replicated on n_gpu GPUs; gpu == gpus[0] */
 	void *gpu;
+	void *gpus[DSB_MAX_GPUS];
+	int n_gpu;
+	void *pool;               /* host thread pool of the read_classify pipeline (pool.c) */
 	/* per-thread_id state (cly_mt.c:1279-1307) */
 	pthread_mutex_t state_mutex;
 	struct dsb_thread_state *states;
@@ -67,24 +72,50 @@ void dsb_index_free_host_tables(dsb_index *ix);
 void dsb_index_host_view(const dsb_index *ix, dsb_dindex_t *d);
 
 /* ------------------------------------------------------------------ reads */
+/* One read as kseq_read leaves it (utils.c:939-977).  The strings are views into the resident
+ * input text, or into the parser's arena (records kseq assembles from several lines); they are
+ * not NUL-terminated in general, and the SAM writer prints them like printf's %s does (up to
+ * the first NUL within the length).  qual == NULL: qual.s was never set ("(null)"); a FASTA
+ * record's qual is its slot's stale quality string (cly_mt.c:229-327 prints qual.s). */
 typedef struct {
-	uint64_t name_off, seq_off, qual_off; /* offsets into the batch text arena */
-	uint32_t seq_l;                       /* kseq seq.l */
-	int32_t qual_null;                    /* qual.s was NULL: printf prints "(null)" */
+	const char *name, *seq, *qual;
+	uint32_t name_l, seq_l, qual_l;
+	uint32_t pad;
 } dsb_rec_t;
 
 typedef struct {
-	char *arena; uint64_t arena_n, arena_m;
 	dsb_rec_t *rec; uint64_t n, m;
+	void *arena_owner; /* arena chunks these records point into (dsb_parse_reads), freed with them */
+	char *text_owner;  /* an owned copy of the input text the records view (dsb_batch_create) */
 } dsb_reads_t;
 
 /* Parse `len` bytes of FASTQ/FASTA text with the semantics of read_reads + kseq_read +
- * kt_pipeline (cly_mt.c:29-43,361-381; utils.c:841-977; kthread.c:114-197). */
+ * kt_pipeline (cly_mt.c:29-43,361-381; utils.c:841-977; kthread.c:114-197).  The records view
+ * `buf`, which must outlive them. */
 int dsb_parse_reads(const char *buf, uint64_t len, dsb_reads_t *out);
+/* The same as a stream of batches over resident text: each call appends whole kt_pipeline
+ * batches until >= max_reads records or >= max_bases bases were added; returns the number of
+ * records appended (0: end of input).  Records stay valid until dsb_parser_free. */
+typedef struct dsb_parser dsb_parser;
+dsb_parser *dsb_parser_new(const char *buf, uint64_t len);
+uint64_t dsb_parser_next(dsb_parser *p, dsb_reads_t *out, uint64_t max_reads, uint64_t max_bases);
+void dsb_parser_stats(const dsb_parser *p, uint64_t *n_fast, uint64_t *n_slow);
+void dsb_parser_free(dsb_parser *p);
 /* read a whole (optionally gzip) file or memory buffer (gzip auto-detected) */
 int dsb_slurp_path(const char *path, char **buf, uint64_t *len);
+int dsb_open_path(const char *path, char **buf, uint64_t *len, uint64_t *unmap_len);
 int dsb_inflate_if_gzip(const char *in, uint64_t in_n, char **buf, uint64_t *len, int *owned);
 void dsb_reads_free(dsb_reads_t *r);
+
+/* ------------------------------------------------------------------ host thread pool */
+/* fn(ctx, task, worker) for every task in [0, n_tasks), spread over the pool's threads and the
+ * calling thread; returns when all are done.  Several threads may run jobs at once. */
+typedef struct dsb_pool dsb_pool;
+dsb_pool *dsb_pool_new(int n_threads);
+int dsb_pool_size(const dsb_pool *p);
+void dsb_pool_run(dsb_pool *p, uint64_t n_tasks, void (*fn)(void *ctx, uint64_t task, int worker), void *ctx);
+void dsb_pool_free(dsb_pool *p);
+int dsb_host_threads(void);
 
 /* ------------------------------------------------------------------ output */
 typedef struct { char *s; uint64_t l, m; } dsb_str;
@@ -94,6 +125,8 @@ void dsb_str_printf(dsb_str *s, const char *fmt, ...);
 enum { DSB_OUT_SAM = 1, DSB_OUT_SAM_FULL = 2, DSB_OUT_DES = 3, DSB_OUT_DES_FULL = 4 };
 void dsb_format_read(dsb_str *out, const dsb_index *ix, const dsb_reads_t *r, uint64_t i,
 		     const dsb_read_out_t *ro, const dsb_hit_out_t *hits, int format, int max_sec_N);
+/* printed length of a %s argument held as (p, n): up to the first NUL */
+static inline uint64_t dsb_cstr_len(const char *p, uint64_t n) { return p ? strnlen(p, n) : 0; }
 
 /* ------------------------------------------------------------------ meta analysis */
 int dsb_meta_analysis(dsb_index *ix, const char *input, uint64_t input_n, char **output, uint64_t *output_n,

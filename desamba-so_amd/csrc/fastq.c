@@ -1,6 +1,6 @@
 /*
  * fastq.c — FASTQ/FASTA parsing with the exact semantics the reference applies on
- * the classify path.
+ * the classify path, as a resumable stream of batches.
  *
  * The reference parses with kseq (src/lib/utils.c:841-977) inside a 3-worker
  * kt_pipeline (src/lib/kthread.c:114-197, src/cly_mt.c:361-381): batch k is read by the
@@ -14,12 +14,23 @@
  *     is empty leaves the pipeline, the others keep reading.
  * SAM_FULL prints qual.s, which for a FASTA record is the slot's previous quality string
  * (or "(null)").
+ *
+ * The input stays resident (the caller's buffer, an mmap'd file, or inflated gzip text) and
+ * records are views into it: a single-line FASTQ record read by a slot whose last_char is 0
+ * (the state every FASTQ record leaves behind) is recognised with memchr and not copied (the
+ * fast path below takes exactly the bytes kseq_read would).  Every other record (FASTA,
+ * multi-line, blank lines, malformed) goes through the byte-level kseq emulation and is
+ * copied into the parser's arena, whose chunks never move and live as long as the parser,
+ * so stale quality strings of earlier batches stay valid.
  */
 #define _GNU_SOURCE
 #include <ctype.h>
+#include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
 #include "dsb_host.h"
@@ -56,6 +67,17 @@ static void ks_refill(kstream_emu *ks)
 	ks->begin = ks->end;
 	ks->end += n;
 	if (n < KS_BUFSIZE) ks->is_eof = 1;
+}
+
+/* move the read position forward to `pos`, refilling windows as ks_getc would have */
+static void ks_seek(kstream_emu *ks, uint64_t pos)
+{
+	while (ks->end < pos) {
+		uint64_t old_end = ks->end;
+		ks_refill(ks);
+		if (ks->end == old_end) break;
+	}
+	ks->begin = pos;
 }
 
 static int ks_getc(kstream_emu *ks) /* utils.c:890-900 */
@@ -107,7 +129,8 @@ static int64_t ks_getuntil2(kstream_emu *ks, int delimiter, kstr *str, int *dret
 
 typedef struct {
 	int last_char;
-	int64_t qual_rec; /* record index whose qual string this slot's qual.s holds, -1 = NULL */
+	const char *qual; /* the slot's qual.s (a stale one for FASTA records); NULL = never set */
+	uint32_t qual_l;
 } slot_state;
 
 typedef struct { kstr name, comment, seq, qual; } kseq_bufs;
@@ -145,78 +168,252 @@ static int64_t kseq_read_emu(kstream_emu *ks, slot_state *st, kseq_bufs *b, int 
 	return (int64_t)b->seq.l;
 }
 
-static uint64_t arena_put(dsb_reads_t *r, const char *s, uint64_t n)
+/* The same record read by a slot whose last_char is 0, when it is one single-line FASTQ
+ * record ("@name...\nSEQ\n+...\nQUAL\n", |QUAL| == |SEQ|): the views kseq_read would have
+ * copied, without copying.  Returns 1 and advances the stream, or 0 (nothing consumed) when
+ * the record is anything else — the byte-level emulation then reads it. */
+static int fastq_view(kstream_emu *ks, dsb_rec_t *rec)
 {
-	if (r->arena_n + n + 1 > r->arena_m) {
-		uint64_t m = r->arena_m ? r->arena_m : (1u << 20);
-		while (m < r->arena_n + n + 1) m <<= 1;
-		r->arena = realloc(r->arena, m);
-		r->arena_m = m;
+	const char *buf = (const char *)ks->buf;
+	uint64_t len = ks->len, p = ks->begin;
+	while (p < len && buf[p] != '@' && buf[p] != '>') p++; /* kseq's header scan */
+	if (p >= len || buf[p] != '@') return 0;
+	uint64_t h = p + 1;
+	const char *nl = memchr(buf + h, '\n', len - h);
+	if (!nl) return 0;
+	uint64_t e = h;
+	while (!isspace((unsigned char)buf[e])) e++; /* name: up to the first isspace (<= the '\n') */
+	uint64_t s = (uint64_t)(nl - buf) + 1, plus;
+	if (s >= len) return 0;
+	uint32_t seq_l = 0;
+	char c = buf[s];
+	if (c == '+') {
+		plus = s;
+	} else {
+		if (c == '>' || c == '@' || c == '\n') return 0; /* FASTA, or a blank line kseq folds in */
+		const char *nl2 = memchr(buf + s, '\n', len - s);
+		if (!nl2) return 0;
+		plus = (uint64_t)(nl2 - buf) + 1;
+		if (plus >= len || buf[plus] != '+') return 0; /* multi-line sequence or FASTA */
+		if ((uint64_t)(nl2 - buf) - s > 0xFFFFFFFFull) return 0;
+		seq_l = (uint32_t)((uint64_t)(nl2 - buf) - s);
 	}
-	uint64_t off = r->arena_n;
-	memcpy(r->arena + off, s, n);
-	r->arena[off + n] = 0;
-	r->arena_n += n + 1;
-	return off;
+	const char *nl3 = memchr(buf + plus, '\n', len - plus);
+	if (!nl3) return 0;
+	uint64_t q = (uint64_t)(nl3 - buf) + 1;
+	if (q >= len) return 0;
+	const char *nl4 = memchr(buf + q, '\n', len - q);
+	uint64_t qe = nl4 ? (uint64_t)(nl4 - buf) : len;
+	if (qe - q != seq_l) return 0; /* multi-line or malformed quality */
+	rec->name = buf + h;
+	rec->name_l = (uint32_t)(e - h);
+	rec->seq = buf + s;
+	rec->seq_l = seq_l;
+	rec->qual = buf + q;
+	rec->qual_l = seq_l;
+	ks_seek(ks, nl4 ? qe + 1 : len);
+	return 1;
 }
 
-int dsb_parse_reads(const char *buf, uint64_t len, dsb_reads_t *out)
+/* ------------------------------------------------------------------ arena */
+typedef struct arena_chunk {
+	struct arena_chunk *next;
+	uint64_t n, m;
+	char data[];
+} arena_chunk;
+
+static const char *arena_put(arena_chunk **head, const char *s, uint64_t n)
 {
-	kstream_emu ks = {(const unsigned char *)buf, len, 0, 0, 0};
-	slot_state *slots = calloc((size_t)N_WORKERS * N_NEEDED, sizeof(slot_state));
-	for (int i = 0; i < N_WORKERS * N_NEEDED; i++) slots[i].qual_rec = -1;
+	arena_chunk *c = *head;
+	if (!c || c->n + n + 1 > c->m) {
+		uint64_t m = (uint64_t)4 << 20;
+		if (m < n + 1) m = n + 1;
+		arena_chunk *nc = malloc(sizeof(arena_chunk) + m);
+		nc->next = c;
+		nc->n = 0;
+		nc->m = m;
+		*head = c = nc;
+	}
+	char *p = c->data + c->n;
+	if (n) memcpy(p, s, n);
+	p[n] = 0;
+	c->n += n + 1;
+	return p;
+}
+
+static void arena_free(arena_chunk *c)
+{
+	while (c) {
+		arena_chunk *n = c->next;
+		free(c);
+		c = n;
+	}
+}
+
+/* ------------------------------------------------------------------ parser */
+struct dsb_parser {
+	kstream_emu ks;
+	slot_state *slots;
 	kseq_bufs b;
-	memset(&b, 0, sizeof(b));
 	int64_t widx[N_WORKERS];
 	int alive[N_WORKERS];
-	for (int w = 0; w < N_WORKERS; w++) { widx[w] = w; alive[w] = 1; }
-	int64_t next_index = N_WORKERS;
-	for (;;) {
-		int w = -1;
-		for (int k = 0; k < N_WORKERS; k++)
-			if (alive[k] && (w < 0 || widx[k] < widx[w])) w = k;
-		if (w < 0) break;
-		long nb = 0, total = 0;
-		for (; nb < N_NEEDED && total < MAX_READ_SIZE; nb++) {
-			slot_state *st = slots + (size_t)w * N_NEEDED + nb;
-			int has_qual;
-			int64_t rst = kseq_read_emu(&ks, st, &b, &has_qual);
-			if (rst < 0) break;
-			total += b.seq.l;
-			if (out->n == out->m) {
-				out->m = out->m ? out->m * 2 : 1024;
-				out->rec = realloc(out->rec, out->m * sizeof(dsb_rec_t));
-			}
-			dsb_rec_t *rec = out->rec + out->n;
-			rec->name_off = arena_put(out, b.name.s ? b.name.s : "", b.name.l);
-			rec->seq_off = arena_put(out, b.seq.s, b.seq.l);
-			rec->seq_l = (uint32_t)b.seq.l;
-			if (has_qual) {
-				rec->qual_off = arena_put(out, b.qual.s, b.qual.l);
-				rec->qual_null = 0;
-				st->qual_rec = (int64_t)out->n;
-			} else if (st->qual_rec >= 0) {
-				rec->qual_off = out->rec[st->qual_rec].qual_off; /* stale qual.s */
-				rec->qual_null = 0;
-			} else {
-				rec->qual_off = 0;
-				rec->qual_null = 1;
-			}
-			out->n++;
-		}
-		if (nb == 0) { alive[w] = 0; continue; }
-		widx[w] = next_index++;
+	int64_t next_index;
+	arena_chunk *arena;
+	int fast;
+	uint64_t n_fast, n_slow;
+	int cur_w;               /* worker whose kt batch is being read (-1: none) */
+	long cur_nb, cur_total;  /* its slots used and bases so far */
+};
+
+dsb_parser *dsb_parser_new(const char *buf, uint64_t len)
+{
+	dsb_parser *p = calloc(1, sizeof(*p));
+	p->ks.buf = (const unsigned char *)buf;
+	p->ks.len = len;
+	p->slots = calloc((size_t)N_WORKERS * N_NEEDED, sizeof(slot_state));
+	for (int w = 0; w < N_WORKERS; w++) {
+		p->widx[w] = w;
+		p->alive[w] = 1;
 	}
-	free(slots);
-	free(b.name.s); free(b.comment.s); free(b.seq.s); free(b.qual.s);
+	p->next_index = N_WORKERS;
+	p->cur_w = -1;
+	p->fast = getenv("DSB_PARSE_SLOW") ? 0 : 1;
+	return p;
+}
+
+static void reads_push(dsb_reads_t *out, const dsb_rec_t *r)
+{
+	if (out->n == out->m) {
+		out->m = out->m ? out->m * 2 : 1024;
+		out->rec = realloc(out->rec, out->m * sizeof(dsb_rec_t));
+	}
+	out->rec[out->n++] = *r;
+}
+
+/* Read one record in the kt_pipeline order: worker w (the alive one with the smallest pipeline
+ * index) fills its slots 0, 1, ... until 5000 reads, >= 10 Mbp, or the first kseq_read() < 0
+ * ends its batch (cly_mt.c:29-43); a worker whose batch is empty leaves the pipeline.  The
+ * batch state is kept in the parser, so a GPU batch may end anywhere inside a kt batch.
+ * Returns 1 with *rec filled, 0 at the end of the input. */
+static int parse_one(dsb_parser *p, dsb_rec_t *rec)
+{
+	for (;;) {
+		if (p->cur_w < 0) {
+			int w = -1;
+			for (int k = 0; k < N_WORKERS; k++)
+				if (p->alive[k] && (w < 0 || p->widx[k] < p->widx[w])) w = k;
+			if (w < 0) return 0;
+			p->cur_w = w;
+			p->cur_nb = 0;
+			p->cur_total = 0;
+		}
+		if (p->cur_nb < N_NEEDED && p->cur_total < MAX_READ_SIZE) {
+			slot_state *st = p->slots + (size_t)p->cur_w * N_NEEDED + p->cur_nb;
+			if (p->fast && st->last_char == 0 && fastq_view(&p->ks, rec)) {
+				st->qual = rec->qual;
+				st->qual_l = rec->qual_l;
+				p->cur_total += rec->seq_l;
+				p->cur_nb++;
+				p->n_fast++;
+				return 1;
+			}
+			int has_qual;
+			int64_t rst = kseq_read_emu(&p->ks, st, &p->b, &has_qual);
+			if (rst >= 0) {
+				rec->name = arena_put(&p->arena, p->b.name.s ? p->b.name.s : "", p->b.name.l);
+				rec->name_l = (uint32_t)p->b.name.l;
+				rec->seq = arena_put(&p->arena, p->b.seq.s, p->b.seq.l);
+				rec->seq_l = (uint32_t)p->b.seq.l;
+				if (has_qual) {
+					rec->qual = arena_put(&p->arena, p->b.qual.s, p->b.qual.l);
+					rec->qual_l = (uint32_t)p->b.qual.l;
+					st->qual = rec->qual;
+					st->qual_l = rec->qual_l;
+				} else { /* FASTA: SAM_FULL prints the slot's stale qual.s, or "(null)" */
+					rec->qual = st->qual;
+					rec->qual_l = st->qual_l;
+				}
+				p->cur_total += p->b.seq.l;
+				p->cur_nb++;
+				p->n_slow++;
+				return 1;
+			}
+		}
+		/* the kt batch of worker cur_w ends here */
+		if (p->cur_nb == 0)
+			p->alive[p->cur_w] = 0;
+		else
+			p->widx[p->cur_w] = p->next_index++;
+		p->cur_w = -1;
+	}
+}
+
+uint64_t dsb_parser_next(dsb_parser *p, dsb_reads_t *out, uint64_t max_reads, uint64_t max_bases)
+{
+	uint64_t n0 = out->n, bases = 0;
+	dsb_rec_t rec;
+	while (out->n - n0 < max_reads && bases < max_bases && parse_one(p, &rec)) {
+		reads_push(out, &rec);
+		bases += rec.seq_l;
+	}
+	return out->n - n0;
+}
+
+void dsb_parser_stats(const dsb_parser *p, uint64_t *n_fast, uint64_t *n_slow)
+{
+	*n_fast = p->n_fast;
+	*n_slow = p->n_slow;
+}
+
+void dsb_parser_free(dsb_parser *p)
+{
+	if (!p) return;
+	free(p->slots);
+	free(p->b.name.s); free(p->b.comment.s); free(p->b.seq.s); free(p->b.qual.s);
+	arena_free(p->arena);
+	free(p);
+}
+
+/* Whole input at once.  The records are views into `buf` (which must outlive `out`) and into
+ * an arena `out` owns. */
+int dsb_parse_reads(const char *buf, uint64_t len, dsb_reads_t *out)
+{
+	dsb_parser *p = dsb_parser_new(buf, len);
+	while (dsb_parser_next(p, out, UINT64_MAX, UINT64_MAX));
+	out->arena_owner = p->arena;
+	p->arena = NULL;
+	dsb_parser_free(p);
 	return 0;
 }
 
 void dsb_reads_free(dsb_reads_t *r)
 {
-	free(r->arena);
+	arena_free((arena_chunk *)r->arena_owner);
 	free(r->rec);
+	free(r->text_owner);
 	memset(r, 0, sizeof(*r));
+}
+
+/* ------------------------------------------------------------------ input sources */
+static int inflate_all(gzFile gz, char **buf, uint64_t *len, uint64_t hint)
+{
+	uint64_t m = hint < (1 << 24) ? (1 << 24) : hint, n = 0;
+	char *p = malloc(m);
+	if (!p) return -1;
+	for (;;) {
+		if (m - n < 1 << 20) {
+			m *= 2;
+			char *q = realloc(p, m);
+			if (!q) { free(p); return -1; }
+			p = q;
+		}
+		int k = gzread(gz, p + n, (unsigned)((m - n) > (1u << 30) ? (1u << 30) : (m - n)));
+		if (k <= 0) break;
+		n += (uint64_t)k;
+	}
+	*buf = p;
+	*len = n;
+	return 0;
 }
 
 int dsb_inflate_if_gzip(const char *in, uint64_t in_n, char **buf, uint64_t *len, int *owned)
@@ -235,17 +432,9 @@ int dsb_inflate_if_gzip(const char *in, uint64_t in_n, char **buf, uint64_t *len
 	gzFile gz = gzdopen(dup(fileno(tf)), "r");
 	fclose(tf);
 	if (!gz) return -1;
-	uint64_t m = in_n * 4 + 4096, n = 0;
-	char *p = malloc(m);
-	for (;;) {
-		if (m - n < 1 << 20) { m *= 2; p = realloc(p, m); }
-		int k = gzread(gz, p + n, (unsigned)((m - n) > (1u << 30) ? (1u << 30) : (m - n)));
-		if (k <= 0) break;
-		n += (uint64_t)k;
-	}
+	int rc = inflate_all(gz, buf, len, in_n * 4 + 4096);
 	gzclose(gz);
-	*buf = p;
-	*len = n;
+	if (rc) return -1;
 	*owned = 1;
 	return 0;
 }
@@ -254,16 +443,32 @@ int dsb_slurp_path(const char *path, char **buf, uint64_t *len)
 {
 	gzFile gz = gzopen(path, "r");
 	if (!gz) return -1;
-	uint64_t m = 1 << 24, n = 0;
-	char *p = malloc(m);
-	for (;;) {
-		if (m - n < 1 << 20) { m *= 2; p = realloc(p, m); }
-		int k = gzread(gz, p + n, (unsigned)((m - n) > (1u << 30) ? (1u << 30) : (m - n)));
-		if (k <= 0) break;
-		n += (uint64_t)k;
-	}
+	int rc = inflate_all(gz, buf, len, 0);
 	gzclose(gz);
-	*buf = p;
-	*len = n;
-	return 0;
+	return rc;
+}
+
+/* Input of read_classify in path mode (input_n == (uint64_t)-1, cly_mt.c:1049-1052): a plain
+ * file is mapped, not read (the parser's views point into the mapping); a gzip file is
+ * inflated into memory.  Returns 0; *unmap_len > 0 means munmap(*buf, *unmap_len), else free. */
+int dsb_open_path(const char *path, char **buf, uint64_t *len, uint64_t *unmap_len)
+{
+	*unmap_len = 0;
+	int fd = open(path, O_RDONLY);
+	if (fd < 0) return -1;
+	unsigned char magic[2] = {0, 0};
+	struct stat sb;
+	if (fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode) && sb.st_size > 0 &&
+	    pread(fd, magic, 2, 0) == 2 && !(magic[0] == 0x1f && magic[1] == 0x8b)) {
+		void *m = mmap(NULL, (size_t)sb.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+		close(fd);
+		if (m == MAP_FAILED) return dsb_slurp_path(path, buf, len);
+		madvise(m, (size_t)sb.st_size, MADV_SEQUENTIAL);
+		*buf = m;
+		*len = (uint64_t)sb.st_size;
+		*unmap_len = (uint64_t)sb.st_size;
+		return 0;
+	}
+	close(fd);
+	return dsb_slurp_path(path, buf, len);
 }

@@ -36,8 +36,8 @@ typedef struct {
 	uint64_t stats[DSB_N_STATS]; /* work counters DSB_ST_*: [32*ph, 32*ph+32) phase ph, [288,320) k_classB */
 } dsb_gpu_timing;
 
-/* Upload the index to `device` (-1: DSB_DEVICE env var, else the current HIP device).
- * Returns 0; on failure fills err. */
+/* Upload the index to `device`; -1: the DSB_DEVICES list ("all" or "0,1,..."), else the
+ * DSB_DEVICE env var, else the current HIP device.  Returns 0; on failure fills err. */
 int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn);
 void dsb_gpu_free(dsb_index *ix);
 
@@ -64,6 +64,26 @@ void dsb_gpu_batch_free(dsb_index *ix, dsb_gpu_batch *b);
  * first): the per-read taxa come from classB (dsb_read_taxon); weights[i] (host, NULL = 1) */
 int dsb_gpu_batch_counts(dsb_index *ix, dsb_gpu_batch *b, const uint32_t *weights, uint64_t *dev_counts,
 			 uint64_t n_counts, char *err, size_t errn);
+
+/* The carried max_read_l of a stream of batches (the reference's one buffer pool per
+ * read_classify thread, cly.c:2953): carry_in blocks until the batch before has published its
+ * carry-out; carry_out publishes this batch's (called after its part A, before its part B). */
+typedef struct {
+	int (*carry_in)(void *ctx);
+	void (*carry_out)(void *ctx, int carry);
+	void *ctx;
+} dsb_carry_hooks;
+int dsb_gpu_batch_run_chain(dsb_index *ix, dsb_gpu_batch *b, int stats_on, const dsb_carry_hooks *hooks,
+			    dsb_gpu_timing *timing, char *err, size_t errn);
+/* Upload reads to GPU `slot` of the index (0 .. n_devices-1) through pinned staging on the
+ * device's copy stream, without its run lock (overlaps the batch before).  The records' bases
+ * are gathered by `pool`; *ms_gather += the gather time.  Recycle the batch when done. */
+int dsb_gpu_batch_stage(dsb_index *ix, int slot, const dsb_reads_t *reads, dsb_pool *pool, dsb_gpu_batch **b,
+			double *ms_gather, char *err, size_t errn);
+void dsb_gpu_batch_recycle(dsb_index *ix, dsb_gpu_batch *b);
+int dsb_gpu_batch_device(const dsb_index *ix, const dsb_gpu_batch *b);
+int dsb_gpu_n_devices(const dsb_index *ix);
+int dsb_gpu_device_id(const dsb_index *ix, int slot);
 
 /* Number of visible devices (0 if HIP has none). */
 int dsb_gpu_device_count(void);

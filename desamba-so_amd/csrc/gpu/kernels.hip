@@ -146,7 +146,8 @@ __global__ __launch_bounds__(64) void k_classB(const dsb_dindex_t *__restrict__ 
 	hit_off[r] = off;
 	o.hit_off = off;
 	ro[r] = o;
-	tid_out[r] = dsb_read_taxon(stage, o.n_hit, ix->ref_tid, ix->p_tid, ix->max_tid);
+	/* per-read taxon (meta_analysis' rule); an index loaded without a taxonomy reports 0 */
+	tid_out[r] = (ix->ref_tid && ix->p_tid) ? dsb_read_taxon(stage, o.n_hit, ix->ref_tid, ix->p_tid, ix->max_tid) : 0;
 	if (STATS)
 		for (int k = 0; k < DSB_ST_N; k++)
 			atomicAdd(gstats + DSB_STATS_B + k, (unsigned long long)st[k]);
@@ -233,8 +234,10 @@ struct dbuf {
 	~dbuf() { release(); }
 };
 
+struct dsb_gpu_batch;
 struct dsb_gpu_dev {
 	int device;
+	int slot;                /* index in dsb_index.gpus */
 	hipStream_t stream;
 	hipStream_t stream2;     /* scoring of the reads that skip slow seeding, beside the slow phases */
 	hipEvent_t ev_a, ev_b, ev_fork, ev_r0, ev_r1;
@@ -245,6 +248,16 @@ struct dsb_gpu_dev {
 	std::vector<void *> allocs;
 	dbuf ws_off, scale, ws, wsr, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2, woA, woB;
 	uint32_t tag = 0;        /* phase-launch counter: the seeding sp_set slot tags (dsb_hset_tag) */
+	/* streamed batches (read_classify pipeline): uploads on their own stream through pinned
+	 * staging, under their own lock, beside the kernels of the batch before */
+	hipStream_t cstream;
+	pthread_mutex_t umu;
+	void *pin[2] = {nullptr, nullptr};
+	size_t pin_cap[2] = {0, 0};
+	hipEvent_t pin_ev[2];
+	int pin_used[2] = {0, 0};
+	int pin_next = 0;
+	std::vector<dsb_gpu_batch *> spare; /* recycled batches: their device buffers are reused, never freed mid-pipeline */
 };
 
 template <typename T>
@@ -268,29 +281,18 @@ extern "C" int dsb_gpu_device_count(void)
 	return n;
 }
 
-extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
+static int dev_init(dsb_index *ix, int device, dsb_gpu_dev **out, char *err, size_t errn)
 {
-	int ndev = 0;
-	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
-		snprintf(err, errn, "no HIP device visible: the deSAMBA MI355X classify path has no CPU fallback");
-		return -1;
-	}
-	if (device < 0) {
-		const char *e = getenv("DSB_DEVICE");
-		if (e)
-			device = atoi(e);
-		else
-			HIP_OK(hipGetDevice(&device));
-	}
-	if (device >= ndev) {
-		snprintf(err, errn, "device %d out of range (%d visible)", device, ndev);
-		return -1;
-	}
 	HIP_OK(hipSetDevice(device));
 	dsb_gpu_dev *g = new dsb_gpu_dev();
+	*out = g;
 	g->device = device;
 	pthread_mutex_init(&g->mu, NULL);
+	pthread_mutex_init(&g->umu, NULL);
 	HIP_OK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+	HIP_OK(hipStreamCreateWithFlags(&g->cstream, hipStreamNonBlocking));
+	for (int k = 0; k < 2; k++)
+		HIP_OK(hipEventCreateWithFlags(&g->pin_ev[k], hipEventDisableTiming));
 	HIP_OK(hipEventCreate(&g->ev_a));
 	HIP_OK(hipEventCreate(&g->ev_b));
 	{ /* the split-off scoring yields to the slow phases */
@@ -347,16 +349,87 @@ extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
 	const dsb_dindex_t *dptr;
 	if (upload(g, &h, 1, &dptr, err, errn)) return -1;
 	g->d = (dsb_dindex_t *)dptr;
-	ix->gpu = g;
 	return 0;
 }
 
-extern "C" void dsb_gpu_free(dsb_index *ix)
+static void dev_free(dsb_gpu_dev *g);
+
+/* The devices the index is replicated on: DSB_DEVICES ("all" or a comma list), else
+ * DSB_DEVICE, else the current HIP device; `device` >= 0 forces that one. */
+extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
 {
-	dsb_gpu_dev *g = (dsb_gpu_dev *)ix->gpu;
-	if (!g)
-		return;
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+		snprintf(err, errn, "no HIP device visible: the deSAMBA MI355X classify path has no CPU fallback");
+		return -1;
+	}
+	int devs[DSB_MAX_GPUS], n = 0;
+	const char *list = getenv("DSB_DEVICES");
+	if (device < 0 && list && *list) {
+		if (!strcmp(list, "all")) {
+			for (int d = 0; d < ndev && n < DSB_MAX_GPUS; d++)
+				devs[n++] = d;
+		} else {
+			for (const char *q = list; *q && n < DSB_MAX_GPUS;) {
+				char *e;
+				long d = strtol(q, &e, 10);
+				if (e == q)
+					break;
+				devs[n++] = (int)d;
+				q = *e == ',' ? e + 1 : e;
+			}
+		}
+	}
+	if (n == 0) {
+		if (device < 0) {
+			const char *e = getenv("DSB_DEVICE");
+			if (e)
+				device = atoi(e);
+			else
+				HIP_OK(hipGetDevice(&device));
+		}
+		devs[n++] = device;
+	}
+	for (int k = 0; k < n; k++)
+		if (devs[k] < 0 || devs[k] >= ndev) {
+			snprintf(err, errn, "device %d out of range (%d visible)", devs[k], ndev);
+			return -1;
+		}
+	for (int k = 0; k < n; k++) {
+		dsb_gpu_dev *g = nullptr;
+		if (dev_init(ix, devs[k], &g, err, errn)) {
+			if (g)
+				dev_free(g);
+			for (int j = 0; j < k; j++)
+				dev_free((dsb_gpu_dev *)ix->gpus[j]);
+			ix->n_gpu = 0;
+			ix->gpu = NULL;
+			return -1;
+		}
+		g->slot = k;
+		ix->gpus[k] = g;
+	}
+	ix->n_gpu = n;
+	ix->gpu = ix->gpus[0];
+	return 0;
+}
+
+static void batch_destroy(dsb_gpu_batch *b);
+
+static void dev_free(dsb_gpu_dev *g)
+{
 	hipSetDevice(g->device);
+	hipDeviceSynchronize();
+	for (dsb_gpu_batch *b : g->spare)
+		batch_destroy(b);
+	g->spare.clear();
+	for (int k = 0; k < 2; k++) {
+		if (g->pin[k])
+			hipHostFree(g->pin[k]);
+		hipEventDestroy(g->pin_ev[k]);
+	}
+	hipStreamDestroy(g->cstream);
+	pthread_mutex_destroy(&g->umu);
 	for (void *p : g->allocs)
 		hipFree(p);
 	dbuf *bs[] = {&g->ws_off, &g->scale, &g->ws, &g->wsr, &g->order, &g->word_off, &g->ro, &g->mrl, &g->hits,
@@ -372,7 +445,21 @@ extern "C" void dsb_gpu_free(dsb_index *ix)
 	hipStreamDestroy(g->stream);
 	pthread_mutex_destroy(&g->mu);
 	delete g;
+}
+
+extern "C" void dsb_gpu_free(dsb_index *ix)
+{
+	for (int k = 0; k < ix->n_gpu; k++)
+		if (ix->gpus[k])
+			dev_free((dsb_gpu_dev *)ix->gpus[k]);
+	ix->n_gpu = 0;
 	ix->gpu = NULL;
+}
+
+extern "C" int dsb_gpu_n_devices(const dsb_index *ix) { return ix->n_gpu; }
+extern "C" int dsb_gpu_device_id(const dsb_index *ix, int slot)
+{
+	return slot >= 0 && slot < ix->n_gpu ? ((dsb_gpu_dev *)ix->gpus[slot])->device : -1;
 }
 
 static double now_ms(void)
@@ -484,7 +571,10 @@ static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, 
 		hipDeviceSynchronize();
 		g->tag = 1;
 		if (g->ws.p)
-			hipMemset(g->ws.p, 0, g->ws.cap);
+			hipMemsetAsync(g->ws.p, 0, g->ws.cap, s);
+		if (g->wsr.p) /* the retry buffer holds tagged sp_set slots too */
+			hipMemsetAsync(g->wsr.p, 0, g->wsr.cap, s);
+		hipStreamSynchronize(s);
 	}
 	uint32_t tag = g->tag;
 	if (wave)
@@ -499,6 +589,9 @@ static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, 
 
 /* a batch of reads resident in HBM (sequences only) + its results */
 struct dsb_gpu_batch {
+	int slot = 0;                /* device (dsb_index.gpus[slot]) holding the reads */
+	hipEvent_t up_ev = nullptr;  /* the upload of a streamed batch (dsb_gpu_batch_stage) */
+	int up_pending = 0;
 	uint64_t n = 0, tot = 0;
 	std::vector<uint32_t> len;
 	std::vector<uint64_t> seq_off;
@@ -517,6 +610,11 @@ static const std::vector<uint32_t> &chunk_order(dsb_gpu_batch *b, uint64_t cb, u
 	for (size_t k = 0; k < b->ord.size(); k++)
 		if (b->ord_cb[k] == cb && b->ord_ce[k] == ce)
 			return b->ord[k];
+	if (cb == 0) { /* a new partition of the batch (the workspace budget changed): drop the old one */
+		b->ord.clear();
+		b->ord_cb.clear();
+		b->ord_ce.clear();
+	}
 	std::vector<uint32_t> order(ce - cb);
 	for (uint32_t i = 0; i < ce - cb; i++) order[i] = i;
 	const std::vector<uint32_t> &len = b->len;
@@ -549,7 +647,7 @@ static int batch_upload(dsb_gpu_dev *g, const dsb_reads_t *reads, dsb_gpu_batch 
 	double th = now_ms();
 	std::vector<uint8_t> stage(tot + 16); /* pack the bases (the arena also holds names/quals) */
 	for (uint64_t i = 0; i < n; i++)
-		memcpy(stage.data() + b->seq_off[i], reads->arena + reads->rec[i].seq_off, b->len[i]);
+		memcpy(stage.data() + b->seq_off[i], reads->rec[i].seq, b->len[i]);
 	HIP_OK(hipMemcpyAsync(b->seq.p, stage.data(), tot, hipMemcpyHostToDevice, s));
 	HIP_OK(hipMemcpyAsync(b->d_seq_off.p, b->seq_off.data(), 8 * n, hipMemcpyHostToDevice, s));
 	HIP_OK(hipMemcpyAsync(b->d_len.p, b->len.data(), 4 * n, hipMemcpyHostToDevice, s));
@@ -683,18 +781,29 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 }
 
 static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on,
-		     dsb_gpu_timing &T, char *err, size_t errn)
+		     dsb_gpu_timing &T, char *err, size_t errn, const dsb_carry_hooks *hooks = nullptr)
 {
 	HIP_OK(hipSetDevice(g->device));
 	hipStream_t s = g->stream;
+	if (b->up_pending) { /* a streamed batch: its bases are still on the way on the copy stream */
+		HIP_OK(hipStreamWaitEvent(s, b->up_ev, 0));
+		b->up_pending = 0;
+	}
 	uint64_t n = b->n;
 	const std::vector<uint32_t> &len = b->len;
 	T.n_reads = n;
 	T.n_bases = b->tot;
 	b->ro.assign(n, dsb_read_out_t());
 	b->hits.clear();
-	if (n == 0)
+	if (n == 0) {
+		if (hooks) { /* keep the carry chain of a stream going */
+			int c = hooks->carry_in ? hooks->carry_in(hooks->ctx) : *max_read_l;
+			if (hooks->carry_out)
+				hooks->carry_out(hooks->ctx, c);
+			*max_read_l = c;
+		}
 		return 0;
+	}
 	if (b->d_tid.ensure(4 * n + 4, err, errn) || g->scale.ensure(4 * n + 4, err, errn) ||
 	    g->ro.ensure(sizeof(dsb_read_out_t) * n + 64, err, errn) ||
 	    g->mrl.ensure(4 * n + 4, err, errn) || g->hit_off.ensure(4 * n + 4, err, errn) ||
@@ -967,7 +1076,11 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				dsb_debug_dump(stderr, &w, "gpuA");
 			}
 		}
-		/* ---- max_read_l carry (src/cly.c:2953): prefix max over reads reaching the update */
+		/* ---- max_read_l carry (src/cly.c:2953): prefix max over reads reaching the update; a
+		 * streamed batch takes its carry-in from the batch before it (possibly on another GPU)
+		 * once its own part A is done, and hands its carry-out on before its part B */
+		if (cb == 0 && hooks && hooks->carry_in)
+			carry = hooks->carry_in(hooks->ctx);
 		uint64_t worst = 0;
 		for (uint32_t i = 0; i < cn; i++) {
 			if (h_ro[cb + i].reached_update && (int)len[cb + i] > carry)
@@ -975,6 +1088,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			mrl[cb + i] = carry;
 			worst += h_ro[cb + i].n_hit;
 		}
+		if (ce == n && hooks && hooks->carry_out)
+			hooks->carry_out(hooks->ctx, carry);
 		HIP_OK(hipMemcpyAsync(g->mrl.p, mrl.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
 		if (g->hits.ensure(sizeof(dsb_hit_out_t) * worst + 4096, err, errn))
 			return -1;
@@ -1023,10 +1138,15 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	return 0;
 }
 
+static dsb_gpu_dev *dev_of(const dsb_index *ix, int slot)
+{
+	return slot >= 0 && slot < ix->n_gpu ? (dsb_gpu_dev *)ix->gpus[slot] : nullptr;
+}
+
 extern "C" int dsb_gpu_batch_upload(dsb_index *ix, const dsb_reads_t *reads, dsb_gpu_batch **out, dsb_gpu_timing *tm,
 				    char *err, size_t errn)
 {
-	dsb_gpu_dev *g = (dsb_gpu_dev *)ix->gpu;
+	dsb_gpu_dev *g = dev_of(ix, 0);
 	if (!g) {
 		snprintf(err, errn, "index not resident on a GPU (dsb_gpu_init not called)");
 		return -1;
@@ -1050,10 +1170,10 @@ extern "C" int dsb_gpu_batch_upload(dsb_index *ix, const dsb_reads_t *reads, dsb
 	return 0;
 }
 
-extern "C" int dsb_gpu_batch_run(dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on, dsb_gpu_timing *tm,
-				 char *err, size_t errn)
+static int run_locked(dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on, dsb_gpu_timing *tm,
+		      const dsb_carry_hooks *hooks, char *err, size_t errn)
 {
-	dsb_gpu_dev *g = (dsb_gpu_dev *)ix->gpu;
+	dsb_gpu_dev *g = dev_of(ix, b->slot);
 	if (!g) {
 		snprintf(err, errn, "index not resident on a GPU (dsb_gpu_init not called)");
 		return -1;
@@ -1062,7 +1182,7 @@ extern "C" int dsb_gpu_batch_run(dsb_index *ix, dsb_gpu_batch *b, int *max_read_
 	dsb_gpu_timing T;
 	memset(&T, 0, sizeof(T));
 	pthread_mutex_lock(&g->mu);
-	int rc = batch_run(g, ix, b, max_read_l, stats_on, T, err, errn);
+	int rc = batch_run(g, ix, b, max_read_l, stats_on, T, err, errn, hooks);
 	pthread_mutex_unlock(&g->mu);
 	T.ms_total = now_ms() - t0;
 	if (tm) {
@@ -1073,16 +1193,161 @@ extern "C" int dsb_gpu_batch_run(dsb_index *ix, dsb_gpu_batch *b, int *max_read_
 	return rc;
 }
 
+extern "C" int dsb_gpu_batch_run(dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on, dsb_gpu_timing *tm,
+				 char *err, size_t errn)
+{
+	return run_locked(ix, b, max_read_l, stats_on, tm, nullptr, err, errn);
+}
+
+extern "C" int dsb_gpu_batch_run_chain(dsb_index *ix, dsb_gpu_batch *b, int stats_on, const dsb_carry_hooks *hooks,
+				       dsb_gpu_timing *tm, char *err, size_t errn)
+{
+	int mrl = 0;
+	return run_locked(ix, b, &mrl, stats_on, tm, hooks, err, errn);
+}
+
+/* ---- streamed batches (the read_classify pipeline) */
+struct gather_ctx {
+	const dsb_reads_t *reads;
+	const uint64_t *seq_off;
+	uint8_t *dst;
+	uint64_t per_task;
+};
+
+static void gather_task(void *c_, uint64_t t, int worker)
+{
+	(void)worker;
+	const gather_ctx *c = (const gather_ctx *)c_;
+	uint64_t lo = t * c->per_task, hi = lo + c->per_task;
+	if (hi > c->reads->n)
+		hi = c->reads->n;
+	for (uint64_t i = lo; i < hi; i++)
+		memcpy(c->dst + c->seq_off[i], c->reads->rec[i].seq, c->reads->rec[i].seq_l);
+}
+
+/* Upload `reads` to GPU `slot` without the device's run lock: the bases are gathered from the
+ * record views into pinned staging by the host pool, then copied on the device's copy stream,
+ * so this overlaps the kernels of the batch before.  The batch comes from the device's spare
+ * list when there is one (no hipMalloc / hipFree in steady state). */
+extern "C" int dsb_gpu_batch_stage(dsb_index *ix, int slot, const dsb_reads_t *reads, dsb_pool *pool,
+				   dsb_gpu_batch **out, double *ms_gather, char *err, size_t errn)
+{
+	dsb_gpu_dev *g = dev_of(ix, slot);
+	if (!g) {
+		snprintf(err, errn, "no GPU slot %d", slot);
+		return -1;
+	}
+	HIP_OK(hipSetDevice(g->device));
+	pthread_mutex_lock(&g->umu);
+	int rc = -1;
+	dsb_gpu_batch *b = nullptr;
+	do {
+		if (!g->spare.empty()) {
+			b = g->spare.back();
+			g->spare.pop_back();
+		} else {
+			b = new dsb_gpu_batch();
+			if (hipEventCreateWithFlags(&b->up_ev, hipEventDisableTiming) != hipSuccess) {
+				snprintf(err, errn, "hipEventCreate failed");
+				break;
+			}
+		}
+		b->slot = slot;
+		b->ord.clear();
+		b->ord_cb.clear();
+		b->ord_ce.clear();
+		uint64_t n = reads->n, tot = 0;
+		b->n = n;
+		b->len.resize(n);
+		b->seq_off.resize(n);
+		for (uint64_t i = 0; i < n; i++) {
+			b->seq_off[i] = tot;
+			b->len[i] = reads->rec[i].seq_l;
+			tot += b->len[i];
+		}
+		b->tot = tot;
+		if (b->seq.ensure(tot + 16, err, errn) || b->d_seq_off.ensure(8 * n + 8, err, errn) ||
+		    b->d_len.ensure(4 * n + 4, err, errn))
+			break;
+		/* pinned staging k: free once its last copy has completed */
+		int k = g->pin_next;
+		g->pin_next ^= 1;
+		if (g->pin_used[k] && hipEventSynchronize(g->pin_ev[k]) != hipSuccess) {
+			snprintf(err, errn, "staging event failed");
+			break;
+		}
+		size_t need = tot + 12 * n + 64;
+		if (need > g->pin_cap[k]) {
+			if (g->pin[k])
+				hipHostFree(g->pin[k]);
+			g->pin[k] = nullptr;
+			g->pin_cap[k] = 0;
+			size_t c = need + need / 4;
+			if (hipHostMalloc(&g->pin[k], c, hipHostMallocDefault) != hipSuccess) {
+				snprintf(err, errn, "hipHostMalloc(%zu) failed", c);
+				break;
+			}
+			g->pin_cap[k] = c;
+		}
+		double t0 = now_ms();
+		uint8_t *pin = (uint8_t *)g->pin[k];
+		gather_ctx gc = {reads, b->seq_off.data(), pin, 0};
+		gc.per_task = n / (uint64_t)(4 * dsb_pool_size(pool)) + 1;
+		dsb_pool_run(pool, (n + gc.per_task - 1) / gc.per_task, gather_task, &gc);
+		uint8_t *meta = pin + ((tot + 15) & ~(uint64_t)15);
+		memcpy(meta, b->seq_off.data(), 8 * n);
+		memcpy(meta + 8 * n, b->len.data(), 4 * n);
+		if (ms_gather)
+			*ms_gather += now_ms() - t0;
+		hipStream_t cs = g->cstream;
+		if (hipMemcpyAsync(b->seq.p, pin, tot, hipMemcpyHostToDevice, cs) != hipSuccess ||
+		    hipMemcpyAsync(b->d_seq_off.p, meta, 8 * n, hipMemcpyHostToDevice, cs) != hipSuccess ||
+		    hipMemcpyAsync(b->d_len.p, meta + 8 * n, 4 * n, hipMemcpyHostToDevice, cs) != hipSuccess ||
+		    hipEventRecord(g->pin_ev[k], cs) != hipSuccess || hipEventRecord(b->up_ev, cs) != hipSuccess) {
+			snprintf(err, errn, "batch upload failed");
+			break;
+		}
+		g->pin_used[k] = 1;
+		b->up_pending = 1;
+		rc = 0;
+	} while (0);
+	if (rc && b) {
+		g->spare.push_back(b);
+		b = nullptr;
+	}
+	pthread_mutex_unlock(&g->umu);
+	*out = b;
+	return rc;
+}
+
+/* give a streamed batch back to its device's spare list (results already consumed) */
+extern "C" void dsb_gpu_batch_recycle(dsb_index *ix, dsb_gpu_batch *b)
+{
+	dsb_gpu_dev *g = dev_of(ix, b->slot);
+	pthread_mutex_lock(&g->umu);
+	g->spare.push_back(b);
+	pthread_mutex_unlock(&g->umu);
+}
+
 extern "C" const dsb_read_out_t *dsb_gpu_batch_ro(const dsb_gpu_batch *b) { return b->ro.data(); }
 extern "C" const dsb_hit_out_t *dsb_gpu_batch_hits(const dsb_gpu_batch *b) { return b->hits.data(); }
 extern "C" const int32_t *dsb_gpu_batch_carry(const dsb_gpu_batch *b) { return b->carry.data(); }
 extern "C" uint64_t dsb_gpu_batch_n(const dsb_gpu_batch *b) { return b->n; }
 extern "C" uint64_t dsb_gpu_batch_bases(const dsb_gpu_batch *b) { return b->tot; }
+extern "C" int dsb_gpu_batch_device(const dsb_index *ix, const dsb_gpu_batch *b)
+{
+	dsb_gpu_dev *g = dev_of(ix, b->slot);
+	return g ? g->device : -1;
+}
 
 extern "C" int dsb_gpu_batch_counts(dsb_index *ix, dsb_gpu_batch *b, const uint32_t *weights, uint64_t *dev_counts,
 				    uint64_t n_counts, char *err, size_t errn)
 {
-	dsb_gpu_dev *g = (dsb_gpu_dev *)ix->gpu;
+	dsb_gpu_dev *g = dev_of(ix, b->slot);
+	if (!g) {
+		snprintf(err, errn, "no GPU");
+		return -1;
+	}
 	pthread_mutex_lock(&g->mu);
 	int rc = -1;
 	do {
@@ -1093,6 +1358,11 @@ extern "C" int dsb_gpu_batch_counts(dsb_index *ix, dsb_gpu_batch *b, const uint3
 		}
 		if (!b->d_tid.p) {
 			snprintf(err, errn, "taxon counts before any run of the batch");
+			break;
+		}
+		hipPointerAttribute_t pa;
+		if (hipPointerGetAttributes(&pa, dev_counts) != hipSuccess || pa.device != g->device) {
+			snprintf(err, errn, "taxon counts: the table is not device memory of GPU %d", g->device);
 			break;
 		}
 		hipStream_t s = g->stream;
@@ -1116,14 +1386,21 @@ extern "C" int dsb_gpu_batch_counts(dsb_index *ix, dsb_gpu_batch *b, const uint3
 	return rc;
 }
 
+static void batch_destroy(dsb_gpu_batch *b)
+{
+	if (b->up_ev)
+		hipEventDestroy(b->up_ev);
+	delete b;
+}
+
 extern "C" void dsb_gpu_batch_free(dsb_index *ix, dsb_gpu_batch *b)
 {
-	dsb_gpu_dev *g = ix ? (dsb_gpu_dev *)ix->gpu : nullptr;
+	dsb_gpu_dev *g = ix ? dev_of(ix, b->slot) : nullptr;
 	if (g) {
 		pthread_mutex_lock(&g->mu);
 		hipSetDevice(g->device);
 	}
-	delete b;
+	batch_destroy(b);
 	if (g)
 		pthread_mutex_unlock(&g->mu);
 }

@@ -66,9 +66,12 @@ void dsb_format_read(dsb_str *out, const dsb_index *ix, const dsb_reads_t *r, ui
 		     const dsb_read_out_t *ro, const dsb_hit_out_t *hits, int format, int max_sec_N)
 {
 	const dsb_rec_t *rec = r->rec + i;
-	const char *name = r->arena + rec->name_off;
+	/* the strings are views (not NUL-terminated): printed as %s prints them */
+	const char *name = rec->name;
+	uint64_t name_n = dsb_cstr_len(rec->name, rec->name_l);
 	if (format == DSB_OUT_DES || format == DSB_OUT_DES_FULL) {
-		dsb_str_printf(out, "%s\t%s\t%s\t%ld\tn_rst:[%ld]\tn_anc:[%ld]\t\n", name,
+		dsb_str_put(out, name, name_n);
+		dsb_str_printf(out, "\t%s\t%s\t%ld\tn_rst:[%ld]\tn_anc:[%ld]\t\n",
 			       ro->n_hit ? "CLASSIFY" : "UNCLASSIFY", ro->fast ? "FAST" : "SLOW",
 			       (long)rec->seq_l, (long)ro->n_hit, (long)ro->n_anchor);
 		int rst_cnt = 0;
@@ -82,14 +85,25 @@ void dsb_format_read(dsb_str *out, const dsb_index *ix, const dsb_reads_t *r, ui
 		return;
 	}
 	int full = format == DSB_OUT_SAM_FULL;
-	const char *seq_s = full ? r->arena + rec->seq_off : "*";
-	const char *qual_s = full ? (rec->qual_null ? "(null)" : r->arena + rec->qual_off) : "*";
+	const char *seq_s = "*", *qual_s = "*";
+	uint64_t seq_n = 1, qual_n = 1;
+	if (full) {
+		seq_s = rec->seq;
+		seq_n = dsb_cstr_len(rec->seq, rec->seq_l);
+		if (rec->qual) {
+			qual_s = rec->qual;
+			qual_n = dsb_cstr_len(rec->qual, rec->qual_l);
+		} else {
+			qual_s = "(null)";
+			qual_n = 6;
+		}
+	}
 	if (ro->n_hit == 0) {
-		put_cstr(out, name);
+		dsb_str_put(out, name, name_n);
 		put_cstr(out, "\t4\t*\t0\t0\t*\t*\t0\t0\t");
-		put_cstr(out, seq_s);
+		dsb_str_put(out, seq_s, seq_n);
 		put_cstr(out, "\t");
-		put_cstr(out, qual_s);
+		dsb_str_put(out, qual_s, qual_n);
 		put_cstr(out, "\t\n");
 		return;
 	}
@@ -101,13 +115,13 @@ void dsb_format_read(dsb_str *out, const dsb_index *ix, const dsb_reads_t *r, ui
 		mapQ_PRI = 30;
 	else
 		mapQ_PRI = (int)((uint32_t)(c_s->sum_score - c_s[1].sum_score) << 2);
-	put_cstr(out, name);
+	dsb_str_put(out, name, name_n);
 	dsb_str_printf(out, "\t%d\t%s\t%d\t%d\t%dS%dM%dS\t*\t0\t0\t", flag, ix->ref_name[c_s->ref_ID],
 		       (int)c_s->t_st, mapQ_PRI, (int)c_s->q_st, (int)(c_s->q_ed - c_s->q_st),
 		       (int)(read_l - c_s->q_ed));
-	put_cstr(out, seq_s);
+	dsb_str_put(out, seq_s, seq_n);
 	put_cstr(out, "\t");
-	put_cstr(out, qual_s);
+	dsb_str_put(out, qual_s, qual_n);
 	dsb_str_printf(out, "\tAS:i:%d\t\n", (int)c_s->sum_score);
 	for (int loop = 0; loop <= 1; loop++) {
 		for (uint32_t k = 1; k < ro->n_hit; k++) {
@@ -124,7 +138,7 @@ void dsb_format_read(dsb_str *out, const dsb_index *ix, const dsb_reads_t *r, ui
 				fl += 0x100;
 			}
 			if (!show) continue;
-			put_cstr(out, name);
+			dsb_str_put(out, name, name_n);
 			dsb_str_printf(out, "\t%d\t%s\t%d\t%d\t%d%c%dM%d%c\t*\t0\t0\t*\t*\tAS:i:%d\t\n", fl,
 				       ix->ref_name[c->ref_ID], (int)c->t_st, mapQ, (int)c->q_st, loop == 0 ? 'H' : 'S',
 				       (int)(c->q_ed - c->q_st), (int)(read_l - c->q_ed), loop == 0 ? 'H' : 'S',

@@ -27,7 +27,10 @@ class Timing(C.Structure):
                 ("n_reads", C.c_uint64),
                 ("n_bases", C.c_uint64), ("n_retry", C.c_uint64), ("n_chunks", C.c_uint64),
                 ("seed_positions", C.c_uint64), ("n_launch_dela", C.c_uint64),
-                ("stats", C.c_uint64 * 320)]
+                ("stats", C.c_uint64 * 320),
+                ("ms_parse", C.c_double), ("ms_gather", C.c_double), ("ms_format", C.c_double),
+                ("ms_wait_gpu", C.c_double), ("n_batches", C.c_uint64), ("n_devices", C.c_uint64),
+                ("n_view_records", C.c_uint64), ("n_copied_records", C.c_uint64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("stats", "ms_phase")}
@@ -83,6 +86,10 @@ def lib(path: str | None = None):
     L.dsb_batch_free.argtypes = [vp, vp]
     L.dsb_max_tid.argtypes = [vp]
     L.dsb_max_tid.restype = u64
+    L.dsb_index_devices.argtypes = [vp, C.c_void_p, C.c_int]
+    L.dsb_index_devices.restype = C.c_int
+    L.dsb_parse_dump.argtypes = [C.c_char_p, u64, C.c_int, u64, C.POINTER(C.c_void_p), u64p]
+    L.dsb_parse_dump.restype = C.c_int
     L.dsb_version.restype = C.c_char_p
     L.dsb_device_count.restype = C.c_int
     L.dsb_free.argtypes = [vp]
@@ -137,6 +144,12 @@ class Index:
     def max_tid(self) -> int:
         return int(self.L.dsb_max_tid(self.h))
 
+    def devices(self) -> list[int]:
+        """HIP device ids the index is replicated on (read_classify uses all of them)."""
+        ids = (C.c_int * 16)()
+        n = self.L.dsb_index_devices(self.h, ids, 16)
+        return [ids[k] for k in range(min(n, 16))]
+
     def meta_analysis(self, sam: bytes, flag: int = 0, max_snapshot_len: int = 65536, thread_id: int = 0):
         out, n = C.c_void_p(), C.c_uint64(0)
         snap, sn = C.c_void_p(), C.c_uint64(0)
@@ -148,6 +161,15 @@ class Index:
         if self.h:
             self.L.dsb_unload_index(self.h)
             self.h = None
+
+
+def parse_dump(data: bytes, slow: bool = False, batch_reads: int = 0) -> bytes:
+    """Records the library's FASTQ/FASTA parser yields (host only, no GPU): one
+    "name\tseq_l\tseq\tqual\n" line per record."""
+    L = lib()
+    out, n = C.c_void_p(), C.c_uint64(0)
+    L.dsb_parse_dump(data, len(data), int(slow), batch_reads, C.byref(out), C.byref(n))
+    return _take(L, out, n.value)
 
 
 class Batch:
@@ -205,6 +227,9 @@ class Batch:
         >= max_tid + 1 entries), reduced on the device (dsb_batch_taxon_counts)."""
         import torch
         assert counts.is_cuda and counts.dtype == torch.int64 and counts.is_contiguous()
+        dev = self.ix.devices()[0]
+        if counts.device.index != dev:
+            raise ValueError(f"counts is on cuda:{counts.device.index}, the batch is on GPU {dev}")
         torch.cuda.current_stream().synchronize()  # the library works on its own stream
         if self.L.dsb_batch_taxon_counts(self.ix.h, self.h, flag, counts.data_ptr(), counts.numel()) != 0:
             raise RuntimeError("dsb_batch_taxon_counts failed")

@@ -21,6 +21,9 @@ typedef struct {
 	uint64_t seed_positions; /* k-mer positions probed by k_seed (both strands) */
 	uint64_t n_launch_dela;  /* launches of the scoring kernel k_wave_phase<8> (2 per chunk when split) */
 	uint64_t stats[320];   /* work counters: [32*ph, +32) phase ph of part A, [288,320) k_classB */
+	/* the streaming pipeline of dsb_classify_text / read_classify (host stages, wall times) */
+	double ms_parse, ms_gather, ms_format, ms_wait_gpu;
+	uint64_t n_batches, n_devices, n_view_records, n_copied_records;
 } dsb_timing_t;
 
 /* Classify FASTQ/FASTA text.  format: 1 SAM, 2 SAM_FULL, 3 DES, 4 DES_FULL.
@@ -55,6 +58,16 @@ uint64_t dsb_batch_bases(dsb_batch *b);
 void dsb_batch_free(void *idx, dsb_batch *b);
 /* largest taxid of the loaded taxonomy (+1e6, reference src/cly_mt.c:613) */
 uint64_t dsb_max_tid(void *idx);
+/* the GPUs the index is replicated on (load_index: DSB_DEVICES "all" / "0,1,..", else DSB_DEVICE,
+ * else the current device): writes up to max_ids HIP device ids, returns their number.
+ * read_classify spreads its batches over all of them; the batch API uses the first. */
+int dsb_index_devices(void *idx, int *device_ids, int max_ids);
+
+/* Diagnostics (host only): the records the FASTQ/FASTA parser yields, one "name\tseq_l\tseq\tqual\n"
+ * line each (strings as printf %s prints them); slow: byte-level kseq emulation only;
+ * batch_reads > 0: parse as the streaming pipeline does, in batches. */
+int dsb_parse_dump(const char *text, uint64_t text_n, int slow, uint64_t batch_reads, char **output,
+		   uint64_t *output_n);
 
 const char *dsb_version(void);
 int dsb_device_count(void);

@@ -20,6 +20,8 @@
  *   --dump F     per-read stage dump (seeds, anchors, chains) to file F.
  *   --max-read-l N  initial max_read_l carried into the first read.
  *   --sam        SAM instead of SAM_FULL (SEQ and QUAL printed as '*').
+ *   --des        DES records (the reference's output_one_result_des, src/cly_mt.c:144-185).
+ *   --des-full   DES_FULL records (output_one_result_full, src/cly_mt.c:187-227).
  *
  * usage: ref_classify [opts] <index_dir> <reads.fq>
  */
@@ -56,6 +58,20 @@ void delete_small_score_rst(DA_IDX *idx, cly_r *results, H_SEARCH_DIR *search_di
 void detect_primary(chain_item *hit, uint32_t n_hit, uint32_t read_len);
 void calculate_MAPQ_TABLE(int *Q_MEM, int (*Q_LV)[MAX_LV_R_LEN], double P_E, uint64_t L_REF);
 void output_one_result_sam(DA_IDX *idx, cly_r *p_rst, int output_seq, MAP_opt *o);
+void output_one_result_des(DA_IDX *idx, cly_r *p_rst, MAP_opt *o);
+void output_one_result_full(DA_IDX *idx, cly_r *p_rst, MAP_opt *o);
+
+/* 0: SAM / SAM_FULL (with_seq), 1: DES, 2: DES_FULL */
+static int g_des = 0;
+static void output_one(DA_IDX *idx, cly_r *r, int with_seq, MAP_opt *o)
+{
+	if (g_des == 1)
+		output_one_result_des(idx, r, o);
+	else if (g_des == 2)
+		output_one_result_full(idx, r, o);
+	else
+		output_one_result_sam(idx, r, with_seq, o);
+}
 
 static FILE *g_dump = NULL;
 
@@ -172,6 +188,8 @@ int main(int argc, char **argv)
 		else if (!strcmp(argv[ai], "--dump") && ai + 1 < argc) dump_path = argv[++ai];
 		else if (!strcmp(argv[ai], "--max-read-l") && ai + 1 < argc) max_read_l = atoi(argv[++ai]);
 		else if (!strcmp(argv[ai], "--sam")) with_seq = 0; /* SAM: SEQ/QUAL printed as '*' */
+		else if (!strcmp(argv[ai], "--des")) g_des = 1;
+		else if (!strcmp(argv[ai], "--des-full")) g_des = 2;
 		else { fprintf(stderr, "unknown option %s\n", argv[ai]); return 2; }
 	}
 	if (ai + 2 > argc) {
@@ -240,12 +258,12 @@ int main(int argc, char **argv)
 				b.max_read_l = max_read_l;
 				classify_one(seq, idx, &r, &b);
 				max_read_l = b.max_read_l;
-				output_one_result_sam(idx, &r, with_seq, &o);
+				output_one(idx, &r, with_seq, &o);
 				free(r.hit.a); free(r.anchor_v.a);
 				pool_free(&b);
 			} else {
 				classify_one(seq, idx, shared_r + i, &shared);
-				output_one_result_sam(idx, shared_r + i, with_seq, &o);
+				output_one(idx, shared_r + i, with_seq, &o);
 			}
 			n++;
 		}

@@ -74,7 +74,7 @@ int main(int argc, char **argv)
 	uint64_t n_retry = 0;
 	for (uint64_t i = 0; i < reads.n; i++) {
 		uint32_t L = reads.rec[i].seq_l;
-		const uint8_t *seq = (const uint8_t *)reads.arena + reads.rec[i].seq_off;
+		const uint8_t *seq = (const uint8_t *)reads.rec[i].seq;
 		dsb_read_out_t ro;
 		for (uint32_t scale = DSB_SCALE_UNIT;; scale *= DSB_CAP_RETRY) {
 			dsb_caps_t cap = dsb_default_caps(L, scale);

@@ -59,6 +59,16 @@ def test_full_records_identical_to_reference_t1_on_stable_reads(gpu_index, pyd, 
     assert not bad, bad[:10]
 
 
+@pytest.mark.parametrize("name", ["mixed", "ont"])
+@pytest.mark.parametrize("fmt", ["des", "des_full"])
+def test_des_formats_byte_identical_to_hermetic_reference(gpu_index, pyd, name, fmt):
+    """DES / DES_FULL records (output_one_result_des / _full, reference src/cly_mt.c:144-227)
+    against the hermetic reference's own writers (oracle harness --des / --des-full)."""
+    code = pyd.FMT_DES if fmt == "des" else pyd.FMT_DES_FULL
+    out, _, _ = gpu_index.classify(golden(name + ".fq"), fmt=code)
+    assert out == golden(f"{name}.herm.{fmt}")
+
+
 def test_des_format_matches_reference_t1(gpu_index, pyd):
     out, _, _ = gpu_index.classify(golden("mixed.fq"), fmt=pyd.FMT_DES)
     ref = golden("mixed.t1.des").split(b"\n\n")
@@ -66,6 +76,54 @@ def test_des_format_matches_reference_t1(gpu_index, pyd):
     assert len(ref) == len(got)
     same = sum(a == b for a, b in zip(ref, got))
     assert same >= 0.95 * len(ref)
+
+
+def test_trailing_nul_input_like_main_test_2(gpu_index, fixture_index, tmp_path):
+    """The reference's in-memory consumer passes input_n = fsize + 1, i.e. the text plus its
+    terminating NUL (reference main_test_2.c:73).  With a final newline the NUL is skipped by
+    kseq's header scan; without one it joins the last quality line, whose length then differs
+    from the sequence's and kseq drops that record (utils.c:939-977).  Both against the
+    hermetic reference run on this box over files holding the same bytes."""
+    herm = os.path.join(ROOT, "oracle", "_ref", "herm_classify")
+    if not os.path.exists(herm):
+        pytest.skip("oracle/_ref not built")
+    fq = golden("ont.fq")[:400000]
+    fq = fq[: fq.rindex(b"\n@") + 1]  # whole records
+    for data in (fq + b"\0", fq[:-1] + b"\0"):
+        p = tmp_path / "nul.fq"
+        p.write_bytes(data)
+        ref = subprocess.run([herm, fixture_index, str(p)], capture_output=True, check=True, timeout=300).stdout
+        got = gpu_index.read_classify(data, thread_id=31, thread_num=4)
+        assert got == ref
+    assert gpu_index.read_classify(fq + b"\0", thread_id=32) == gpu_index.read_classify(fq, thread_id=33)
+
+
+def test_concurrent_read_classify_distinct_thread_ids(gpu_index):
+    """Concurrent read_classify calls with distinct thread_ids are part of the contract
+    (reference cly_mt.c:1279-1307, desamba.h:20-21): four host threads at once, each output equal
+    to the serial call's (ctypes releases the GIL, so the calls overlap in the library)."""
+    import threading
+    inputs = [golden(n + ".fq") for n in ("mixed", "ont", "illumina", "ont_long")]
+    serial = [gpu_index.read_classify(d, thread_id=40 + k, thread_num=1) for k, d in enumerate(inputs)]
+    got = [None] * len(inputs)
+    errs = []
+
+    def work(k):
+        try:
+            for it in range(2):  # fresh thread_ids: a thread_id carries max_read_l across calls
+                got[k] = gpu_index.read_classify(inputs[k], thread_id=50 + 10 * it + k, thread_num=1)
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(len(inputs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not errs
+    for k in range(len(inputs)):
+        assert got[k] == serial[k], k
+    assert serial[0] == golden("mixed.herm.sam_full")
 
 
 def test_two_calls_carry_pool_state_like_one_call(gpu_index, pyd):
@@ -257,3 +315,29 @@ def test_overflow_reruns_byte_identical(gpu_index, pyd):
     finally:
         os.environ.pop("DSB_TEST_SCALE0", None)
         os.environ.pop("DSB_WS_BUDGET_MB", None)
+
+
+@pytest.mark.parametrize("reads_per_batch,depth", [("37", "2"), ("500", "3"), ("1", "8")])
+def test_streaming_batches_byte_identical(gpu_index, pyd, reads_per_batch, depth):
+    """read_classify / dsb_classify_text stream the input through GPU batches of at most
+    DSB_PIPE_READS reads (pipeline.c); the carried max_read_l crosses every batch boundary
+    (reference cly.c:2953, one pool per call) and the records come back in input order.  Tiny
+    batches + a shallow or deep pipeline against the hermetic goldens."""
+    os.environ["DSB_PIPE_READS"] = reads_per_batch
+    os.environ["DSB_PIPE_DEPTH"] = depth
+    try:
+        for name in ("mixed", "ont_long", "illumina"):
+            out, t, _ = gpu_index.classify(golden(name + ".fq"), fmt=pyd.FMT_SAM)
+            assert out == golden(name + ".herm.sam"), name
+            assert t["n_batches"] >= 2
+            assert t["n_view_records"] + t["n_copied_records"] == t["n_reads"]
+        assert gpu_index.read_classify(golden("mixed.fq"), thread_id=61) == golden("mixed.herm.sam_full")
+    finally:
+        os.environ.pop("DSB_PIPE_READS", None)
+        os.environ.pop("DSB_PIPE_DEPTH", None)
+
+
+def test_single_line_fastq_records_are_views(gpu_index, pyd):
+    """Plain single-line FASTQ is classified in place: no record is copied by the parser."""
+    _, t, _ = gpu_index.classify(golden("ont.fq"), fmt=pyd.FMT_SAM)
+    assert t["n_view_records"] == 2000 and t["n_copied_records"] == 0

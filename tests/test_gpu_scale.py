@@ -1,0 +1,141 @@
+"""GPU parity beyond the C1 bench workload's defaults: the larger-index parameters of BASELINE
+configs C2-C4, C4's read mix, and one read_classify call spread over several GPU contexts.
+
+* l_ek 17 / MASK_31 / quarter-GB e-kmer tables.  The reference builder switches to them at
+  >= 238.6 M distinct 31-mers (reference src/idx.c:966-996), i.e. RefSeq-scale (C2) indexes.
+  Such an index (the 495 Mbp C2 proxy, data/c2_index.txz, 0.9 GB packed) does not fit the GPU
+  box's 512 MiB upload, so the box rebuilds the C1 proxy's tables at that size with
+  oracle/_ref/ekmer_tables, this repo's restatement of the builder's get_EXIST_kmer, which is
+  byte-identical to the builder's own l_ek-16 tables (fixture, C1) and l_ek-17 tables (C2 proxy:
+  tests/test_oracle_pinned.py, profiles/r03_c2/ekmer_check.txt).  The reference classifier
+  (oracle/_ref/herm_classify) loads that index exactly as it would a builder-made one, and is
+  the oracle on it.
+* BASELINE C4's read mix: 150 bp Illumina-like + ONT-like reads of mean 20 kb, interleaved in a
+  fixed order, after a run of short reads: the carried max_read_l (src/cly.c:2953-2963) switches
+  from the Illumina rules to the long-read rule inside the input, and 20 kb+ reads take the
+  2^15-2^17-bucket read 9-mer hashes (src/cly.c:2160-2219).
+* DSB_DEVICES=0,0: the index loaded twice on one GPU, so read_classify's batches alternate
+  between two device contexts and the carry chain crosses them, as on an 8-GPU node.
+"""
+import os
+import shutil
+import subprocess
+import sys
+import tarfile
+
+import pytest
+
+from conftest import ROOT, golden
+from samutil import compare, groups
+
+pytestmark = pytest.mark.gpu
+
+HERM = os.path.join(ROOT, "oracle", "_ref", "herm_classify")
+GCC = os.path.join(ROOT, "oracle", "_ref", "ref_classify")
+EKTAB = os.path.join(ROOT, "oracle", "_ref", "ekmer_tables")
+C1 = os.path.join(ROOT, "data", "c1_index.txz")
+
+
+def _need(*paths):
+    for p in paths:
+        if not os.path.exists(p):
+            pytest.skip(f"{os.path.relpath(p, ROOT)} absent")
+
+
+@pytest.fixture(scope="module")
+def c1_dir(tmp_path_factory):
+    _need(C1)
+    d = tmp_path_factory.mktemp("c1s")
+    with tarfile.open(C1) as t:
+        t.extractall(d)
+    return str(d)
+
+
+@pytest.fixture(scope="module")
+def lek17_dir(c1_dir, tmp_path_factory):
+    """The C1 proxy with the quarter-GB l_ek-17 / MASK_31 e-kmer tables."""
+    _need(EKTAB)
+    d = tmp_path_factory.mktemp("c1_lek17")
+    for f in os.listdir(c1_dir):
+        if not f.startswith("deSAMBA.exk"):
+            os.symlink(os.path.join(c1_dir, f), os.path.join(d, f))
+    r = subprocess.run([EKTAB, c1_dir, str(1 << 28), str(d)], capture_output=True, text=True, check=True, timeout=300)
+    assert "l_ek 17" in r.stdout, r.stdout
+    with open(os.path.join(d, "deSAMBA.exki"), "rb") as f:
+        assert int.from_bytes(f.read(8), "little") == 1 << 28
+    return str(d)
+
+
+def _sim(index_dir, tmp_path, n, seed, mix):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import simulate
+    genomes = simulate.read_fasta_genomes_from_index(index_dir)
+    if mix == "c4":
+        lead = list(simulate.simulate_reads(genomes, 20, seed + 7, "illumina"))  # short reads first
+        reads = lead + list(simulate.simulate_c4_mix(genomes, n, seed))
+    else:
+        reads = list(simulate.simulate_reads(genomes, n, seed, "ont", 8000))
+    fq = tmp_path / f"{mix}_{seed}.fq"
+    simulate.write_fastq(reads, str(fq))
+    return fq
+
+
+def _check_vs_reference(pyd, index_dir, fq, seed, tag):
+    """T1 on every read, T2 on every read two reference builds agree on, T3 bounded (the
+    uninitialised-memory reads of SURVEY Appendix A H1) — as tests/test_gpu_c1.py."""
+    _need(HERM, GCC)
+    herm = subprocess.run([HERM, "--sam", index_dir, str(fq)], capture_output=True, check=True, timeout=900).stdout
+    t1 = subprocess.run([GCC, "--sam", "--fresh", index_dir, str(fq)], capture_output=True, check=True,
+                        timeout=900).stdout
+    idx = pyd.Index(index_dir)
+    try:
+        out, t, _ = idx.classify(fq.read_bytes(), fmt=1, stats=True)
+    finally:
+        idx.close()
+    r = compare(herm, out)
+    assert r["taxid_mismatch"] == 0 and r["mapped_mismatch"] == 0, (tag, seed, r)
+    gh, gt, go = groups(herm), groups(t1), groups(out)
+    stable = [i for i in range(len(gh)) if gh[i] == gt[i]]
+    assert len(stable) >= 0.9 * len(gh), (tag, seed, len(stable))
+    bad = [gh[i][0] for i in stable if go[i] != gh[i]]
+    assert not bad, (tag, seed, bad[:5])
+    unstable = [gh[i][0] for i in range(len(gh)) if go[i] != gh[i]]
+    assert len(unstable) <= 0.005 * len(gh), (tag, seed, unstable[:5])
+    print(f"{tag} seed {seed}: {len(gh)} reads, {len(stable)} stable, T3 mismatches {len(unstable)}")
+    return t
+
+
+def test_lek17_mask31_index_matches_reference(pyd, lek17_dir, tmp_path):
+    seed = int(os.environ.get("DSB_TEST_SEED", 5151 + int.from_bytes(os.urandom(2), "little")))
+    fq = _sim(lek17_dir, tmp_path, 2000, seed, "ont")
+    t = _check_vs_reference(pyd, lek17_dir, fq, seed, "C1-lek17")
+    assert t["seed_positions"] > 0
+
+
+def test_c4_mix_150bp_20kb_interleaved_matches_reference(pyd, c1_dir, tmp_path):
+    seed = int(os.environ.get("DSB_TEST_SEED", 6161 + int.from_bytes(os.urandom(2), "little")))
+    fq = _sim(c1_dir, tmp_path, 1000, seed, "c4")
+    lens = [len(l) for i, l in enumerate(fq.read_bytes().split(b"\n")) if i % 4 == 1]
+    assert min(lens) == 150 and max(lens) >= 32768  # 2^16+ bucket read hashes
+    _check_vs_reference(pyd, c1_dir, fq, seed, "C4-mix")
+
+
+def test_read_classify_over_two_device_contexts(pyd, fixture_index):
+    """DSB_DEVICES=0,0: batches of one read_classify call alternate between two contexts holding
+    the index; records and the carried max_read_l equal the single-context call."""
+    os.environ["DSB_DEVICES"] = "0,0"
+    os.environ["DSB_PIPE_READS"] = "41"
+    try:
+        idx = pyd.Index(fixture_index)
+        try:
+            assert idx.devices() == [0, 0]
+            assert idx.read_classify(golden("mixed.fq"), thread_id=3) == golden("mixed.herm.sam_full")
+            for name in ("mixed", "ont_long"):
+                out, t, _ = idx.classify(golden(name + ".fq"), fmt=pyd.FMT_SAM)
+                assert out == golden(name + ".herm.sam"), name
+                assert t["n_devices"] == 2 and t["n_batches"] >= 2
+        finally:
+            idx.close()
+    finally:
+        os.environ.pop("DSB_DEVICES", None)
+        os.environ.pop("DSB_PIPE_READS", None)

@@ -32,6 +32,11 @@ for s in mixed ont ont_long illumina; do
 done
 "$REF/deSAMBA" classify -t 1 -f SAM_FULL "$W/idx" "$W/mixed.fq" > "$W/mixed.t1.sam_full" 2>/dev/null
 "$REF/deSAMBA" classify -t 1 -f DES "$W/idx" "$W/mixed.fq" > "$W/mixed.t1.des" 2>/dev/null
+# hermetic DES / DES_FULL (the reference's own output_one_result_des / _full, cly_mt.c:144-227)
+for s in mixed ont; do
+	"$REF/herm_classify" --des "$W/idx" "$W/$s.fq" > "$W/$s.herm.des" 2>/dev/null
+	"$REF/herm_classify" --des-full "$W/idx" "$W/$s.fq" > "$W/$s.herm.des_full" 2>/dev/null
+done
 # reference meta_analysis over the hermetic SAM_FULL of the mixed set (via its own .so)
 gcc -O1 -o "$W/ref_meta" "$ROOT/tools/ref_meta.c" -ldl
 "$W/ref_meta" "$REF/libdesamba.so" "$W/idx" "$W/mixed.herm.sam_full" 0 > "$W/mixed.meta_reads" 2>/dev/null
@@ -39,7 +44,8 @@ gcc -O1 -o "$W/ref_meta" "$ROOT/tools/ref_meta.c" -ldl
 tar -C "$W/idx" -cf - . | xz -T8 -6 > "$G/fixture_index.txz"
 for f in mixed.fq ont.fq ont_long.fq illumina.fq mixed.herm.sam_full mixed.t1.sam_full mixed.t1.des \
 	 mixed.herm.sam ont.herm.sam ont_long.herm.sam illumina.herm.sam \
-	 mixed.t1.sam ont.t1.sam ont_long.t1.sam illumina.t1.sam mixed.meta_reads mixed.meta_bases; do
+	 mixed.t1.sam ont.t1.sam ont_long.t1.sam illumina.t1.sam mixed.meta_reads mixed.meta_bases \
+	 mixed.herm.des mixed.herm.des_full ont.herm.des ont.herm.des_full; do
 	xz -T4 -9 -c "$W/$f" > "$G/$f.xz"
 done
 cp "$W/ref_manifest.json" "$G/fixture_reference.json"

@@ -204,6 +204,17 @@ def simulate_reads(genomes, n_reads, seed, kind="ont", mean_len=8000, sigma=0.5,
         yield name, s, q
 
 
+def simulate_c4_mix(genomes, n_reads, seed, long_mean=20000):
+    """BASELINE config C4's read mix: 150 bp Illumina-like and ONT-like reads (lognormal mean
+    `long_mean`) 1:1 by count, interleaved in a fixed order (even = long, odd = short), since
+    the carried max_read_l makes results order-dependent (reference cly.c:2953)."""
+    ont = simulate_reads(genomes, (n_reads + 1) // 2, seed, "ont", long_mean)
+    ill = simulate_reads(genomes, n_reads // 2, seed + 1, "illumina")
+    for i in range(n_reads):
+        name, s, q = next(ont) if i % 2 == 0 else next(ill)
+        yield f"m{i}_{name}", s, q
+
+
 def write_fastq(reads, path):
     with open(path, "wb") as f:
         for name, s, q in reads:
@@ -235,6 +246,12 @@ PRESETS = {
     "c1": dict(seed=20240602, n_families=25, copies=5, core_len=400000, flank_len=20000,
                decoy_len=5000, n_shared=6, shared_len=5000,
                repeat_specs=((300, 400, 0.01), (150, 3000, 0.005))),
+    # C2-direction proxy: >= 238.6M distinct 31-mers, so the reference builder picks the
+    # quarter-GB e-kmer tables, l_ek 17 and MASK_31 (reference idx.c:966-996), and the BWT
+    # passes 2^28 symbols (many 2^24-symbol occ superblocks)
+    "c2": dict(seed=20240603, n_families=80, copies=4, core_len=1300000, flank_len=120000,
+               decoy_len=5000, n_shared=8, shared_len=5000,
+               repeat_specs=((300, 2000, 0.01), (150, 12000, 0.005))),
 }
 
 
