@@ -265,9 +265,17 @@ def dropin_leg(idx, fq: bytes, n_reads: int, nb: int, batch_sam_full_sha: str | 
     same = None
     if batch_sam_full_sha is not None:
         same = hashlib.sha256(text).hexdigest() == batch_sam_full_sha
+    del text
+    # the same call through dsb_classify_text, for the pipeline's stage times (host wall times)
+    import pydesamba as P
+    _, tm, _ = idx.classify(fq, fmt=P.FMT_SAM_FULL)
+    stages = {k: round(tm[k], 2) for k in ("ms_total", "ms_parse", "ms_gather", "ms_format", "ms_wait_gpu", "ms_classA",
+                                           "ms_seed", "ms_h2d", "ms_d2h")}
+    stages.update({k: int(tm[k]) for k in ("n_batches", "n_devices", "n_view_records", "n_copied_records")})
     return {"value": round(n_reads / secs, 1), "unit": "reads/s", "secs": round(secs, 4),
             "gbases_per_s": round(nb / secs / 1e9, 4), "reads": n_reads, "input_bytes": len(fq),
-            "output_bytes": n.value, "identical_to_batch_records": same,
+            "output_bytes": n.value, "identical_to_batch_records": same, "pipeline": stages,
+            "host_threads": int(os.environ.get("DSB_HOST_THREADS", "0")) or None,
             "what": "read_classify(idx, fastq_text, n, &out, &out_n, 7, 1): parse + H2D + kernels + D2H + "
                     "SAM_FULL formatting, index preloaded"}
 
@@ -313,6 +321,7 @@ def main():
     ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS), help="proxy index (data/<w>_index.txz)")
     ap.add_argument("--mix", default="ont", choices=["ont", "c4"], help="ONT reads, or C4's 150 bp + 20 kb 1:1 mix")
     ap.add_argument("--index", default=None, help="index directory (overrides --workload)")
+    ap.add_argument("--name", default=None, help="workload name for --index")
     ap.add_argument("--cpu-sample", type=int, default=16000, help="reads in the CPU baseline sample (-t nproc)")
     ap.add_argument("--cpu-sample-t1", type=int, default=2000, help="reads in the -t 1 CPU sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -346,7 +355,7 @@ def main():
     import shard
 
     if a.index:
-        index_dir, workload = a.index, os.path.basename(os.path.normpath(a.index))
+        index_dir, workload = a.index, a.name or os.path.basename(os.path.normpath(a.index))
     else:
         index_dir, workload = unpack_index(rank, a.workload)
     if a.mix == "c4":
@@ -415,6 +424,23 @@ def main():
             per_phase[ph] = {"algorithmic_bytes_per_launch": int(b / nl), "avg_launch_ms": round(ms, 3),
                              "launches_per_step": nl,
                              "achieved_GBs": round(b / nl / (ms / 1e3) / 1e9, 3) if ms > 0 else None}
+        # k_seed (the Bloom probes, SURVEY §8d: 1 B per first / second probe) and the island scan
+        # (reads the exist bits k_seed wrote): their counters ride in the island block
+        isl = ts["stats_phase"]["island"]
+        probes = isl["ek1"] + isl["ek2"]
+        sb = probes + 2 * batch.n_bases + ts["seed_positions"] // 8  # probes + both strands' bases + exist bits
+        ms_seed = sum(t["ms_seed"] for t in tms) / a.steps
+        per_phase["seed"] = {"algorithmic_bytes_per_launch": int(sb), "avg_launch_ms": round(ms_seed, 3),
+                             "launches_per_step": 1,
+                             "achieved_GBs": round(sb / (ms_seed / 1e3) / 1e9, 3) if ms_seed > 0 else None,
+                             "probes": probes, "first_probes": isl["ek1"], "second_probes": isl["ek2"],
+                             "sector_bytes_per_launch": 64 * probes,
+                             "sector_GBs": round(64 * probes / (ms_seed / 1e3) / 1e9, 1) if ms_seed > 0 else None,
+                             "note": "k_seed: one 1-byte Bloom probe costs a 64-B sector; sector_GBs is that rate"}
+        ib = ts["seed_positions"] // 8
+        per_phase["island"]["algorithmic_bytes_per_launch"] = int(ib)
+        ms_i = per_phase["island"]["avg_launch_ms"]
+        per_phase["island"]["achieved_GBs"] = round(ib / (ms_i / 1e3) / 1e9, 3) if ms_i > 0 else None
         d = per_phase[dom]
         traffic = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")

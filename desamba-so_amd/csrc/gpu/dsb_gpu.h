@@ -23,6 +23,7 @@ extern "C" {
 #define DSB_TL_STRIDE (1u << 17)
 #define DSB_N_STATS 320 /* 32 counters x (9 phases of part A + k_classB) */
 #define DSB_STATS_B 288
+#define DSB_STATS_SEED 0 /* k_seed's Bloom-probe counters (ek1, ek2): the island phase's block (island itself probes nothing) */
 
 typedef struct {
 	double ms_total;      /* wall time of dsb_gpu_classify, host-measured */

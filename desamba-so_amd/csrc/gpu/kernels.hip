@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void k_encode(const uint8_t *__restrict__ seq,
 __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 					       const uint64_t *__restrict__ ws_off, uint8_t *__restrict__ ws,
 					       const uint64_t *__restrict__ word_off, const uint32_t *__restrict__ sel,
-					       uint32_t n, uint64_t total_waves)
+					       uint32_t n, uint64_t total_waves, unsigned long long *__restrict__ gstats)
 {
 	uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
 	uint32_t lane = threadIdx.x & 63;
@@ -98,16 +98,28 @@ __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ i
 	uint32_t *pre = (uint32_t *)(base + lay.pre) + (strand ? L : 0);
 	(void)pre;
 	uint32_t k = word * 64 + lane;
-	int e = 0;
+	int e = 0, p1 = 0, p2 = 0;
 	if (k < lk) {
 		uint64_t km = dsb_kmer_at(bin + k, l_ek, ix->single_base_max);
 		if (DSB_SEED_PRE)
 			pre[k] = (uint32_t)(km & DSB_PRE_IDX_MASK); /* the seeding's 13-mer prefix (fast / slow J step) */
+		if (gstats) { /* work counters: first / second Bloom probes (get_exist_kmer, src/cly.c:951-967) */
+			p1 = km != 0;
+			p2 = p1 && ((dsb_gld(ix->ek0 + ((dsb_hash64_1(km) & ix->ek_mask) >> 3)) >>
+				     (7 - (dsb_hash64_1(km) & ix->ek_mask & 0x7))) & 1);
+		}
 		e = dsb_exist_kmer(ix, km);
 	}
 	uint64_t bits = __ballot(e);
 	if (lane == 0)
 		ex[word] = bits;
+	if (gstats) {
+		uint64_t b1 = __ballot(p1), b2 = __ballot(p2);
+		if (lane == 0) {
+			atomicAdd(gstats + DSB_STATS_SEED + DSB_ST_EK1, (unsigned long long)__builtin_popcountll(b1));
+			atomicAdd(gstats + DSB_STATS_SEED + DSB_ST_EK2, (unsigned long long)__builtin_popcountll(b2));
+		}
+	}
 }
 
 template <bool STATS>
@@ -814,6 +826,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	if (g->stats.ensure(8 * DSB_N_STATS + tl_bytes, err, errn))
 		return -1;
 	HIP_OK(hipMemsetAsync(g->stats.p, 0, 8 * DSB_N_STATS + tl_bytes, s));
+	/* k_seed's probe counters (stats mode 1) go to the island phase's ek1 / ek2 slots */
+	unsigned long long *sst = stats_on == 1 ? g->stats.as<unsigned long long>() : nullptr;
 	/* DSB_TEST_SCALE0 (tests): start below the default capacities so that reads overflow and
 	 * take the re-run path */
 	uint32_t scale0 = DSB_SCALE_UNIT;
@@ -893,7 +907,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 					hipEventRecord(g->pev[k][0][0], hs[k]);
 					if (htw[k])
 						k_seed<<<(uint32_t)((htw[k] * 64 + 255) / 256), 256, 0, hs[k]>>>(
-							g->d, cl, g->ws_off.as<uint64_t>(), wsb, hwo[k], ho[k], hm[k], htw[k]);
+							g->d, cl, g->ws_off.as<uint64_t>(), wsb, hwo[k], ho[k], hm[k], htw[k], sst);
 					hipEventRecord(g->pev[k][0][1], hs[k]);
 				}
 				for (int ph = 0; ph < DSB_PH_N; ph++)
@@ -926,7 +940,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			hipEventRecord(g->ev_a, s);
 			if (twA)
 				k_seed<<<(uint32_t)((twA * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
-											      g->woA.as<uint64_t>(), oA, h, twA);
+											      g->woA.as<uint64_t>(), oA, h, twA, sst);
 			hipEventRecord(g->ev_fork, s);
 			HIP_OK(hipStreamWaitEvent(g->stream2, g->ev_fork, 0));
 			hipEventRecord(g->ev_r0, g->stream2);
@@ -934,7 +948,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			hipEventRecord(g->ev_r1, g->stream2);
 			if (twB)
 				k_seed<<<(uint32_t)((twB * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
-											      g->woB.as<uint64_t>(), oB, cn - h, twB);
+											      g->woB.as<uint64_t>(), oB, cn - h, twB, sst);
 			HIP_OK(hipGetLastError());
 			hipEventRecord(g->ev_b, s);
 			HIP_OK(hipEventSynchronize(g->ev_b));
@@ -961,7 +975,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		if (tw) {
 			hipEventRecord(g->ev_a, s);
 			k_seed<<<(uint32_t)((tw * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
-										     g->word_off.as<uint64_t>(), nullptr, cn, tw);
+										     g->word_off.as<uint64_t>(), nullptr, cn, tw, sst);
 			T.ms_seed += ev_ms(g);
 			HIP_OK(hipGetLastError());
 		}
@@ -1048,7 +1062,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			k_encode<<<m, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, g->sel.as<uint32_t>(), m);
 			if (tw2)
 				k_seed<<<(uint32_t)((tw2 * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
-											      g->wo2.as<uint64_t>(), g->sel.as<uint32_t>(), m, tw2);
+											      g->wo2.as<uint64_t>(), g->sel.as<uint32_t>(), m, tw2, nullptr);
 			HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
 			for (int ph = 0; ph < DSB_PH_N; ph++)
 				launch_phase(g, ph, false, cl, wsb, g->sel.as<uint32_t>(), m);

@@ -139,3 +139,20 @@ def test_read_classify_over_two_device_contexts(pyd, fixture_index):
     finally:
         os.environ.pop("DSB_DEVICES", None)
         os.environ.pop("DSB_PIPE_READS", None)
+
+
+def test_c2_proxy_matches_reference(pyd, tmp_path):
+    """The genuine C2-direction proxy (tools/simulate.py preset c2: 495 Mbp, 286 M distinct
+    31-mers, made by the reference builder -> l_ek 17, MASK_31, 256 MB e-kmer tables, ~0.5 G BWT
+    rows over 30 occ superblocks).  Too large for the GPU box's upload, so tools/gpu_c2.sh builds
+    it on the box with oracle/_ref/deSAMBA and points DSB_C2_DIR at it; skipped elsewhere."""
+    d = os.environ.get("DSB_C2_DIR")
+    if not d or not os.path.exists(os.path.join(d, "deSAMBA.bwt")):
+        pytest.skip("DSB_C2_DIR not set (tools/gpu_c2.sh builds the C2 proxy on the GPU box)")
+    with open(os.path.join(d, "deSAMBA.exki"), "rb") as f:
+        assert int.from_bytes(f.read(8), "little") == 1 << 28  # the builder chose l_ek 17 / MASK_31
+    seed = int(os.environ.get("DSB_TEST_SEED", 7171 + int.from_bytes(os.urandom(2), "little")))
+    fq = _sim(d, tmp_path, 2000, seed, "ont")
+    _check_vs_reference(pyd, d, fq, seed, "C2-proxy")
+    fq4 = _sim(d, tmp_path, 600, seed + 1, "c4")
+    _check_vs_reference(pyd, d, fq4, seed + 1, "C2-proxy-C4-mix")
