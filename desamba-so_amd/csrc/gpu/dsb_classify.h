@@ -2365,9 +2365,54 @@ DSB_HD dsb_spd_t *dsb_push_sms(dsb_read_ws *w)
 /* MEM_search: the byte loop `len < max && *q++ == *t++` (or `*q-- == *t--`) compared 8 bytes
  * per step: the first differing byte is the lowest (forward) / highest (backward) set byte of
  * the XOR.  Same result as the byte loop for every max >= 0. */
+#ifndef DSB_MEM_WORDS
+#define DSB_MEM_WORDS 1
+#endif
+/* W consecutive unaligned u64 at p from W + 1 aligned loads, all issued before any is used */
+template <int W>
+DSB_HD void dsb_ldwu(const uint8_t *p, uint64_t *out)
+{
+	uint32_t o = (uint32_t)((uintptr_t)p & 7), sh = o * 8;
+	const uint64_t *b = (const uint64_t *)(p - o);
+	uint64_t v[W + 1];
+	for (int k = 0; k <= W; k++) v[k] = b[k];
+	for (int k = 0; k < W; k++) out[k] = sh ? (v[k] >> sh) | (v[k + 1] << (64 - sh)) : v[k];
+}
+
 DSB_HD int dsb_MEM_search(const uint8_t *q, const uint8_t *t, int forward, int max)
 {
 	int len = 0;
+	if (DSB_MEM_WORDS > 1 && max > 8) {
+		/* long extensions: DSB_MEM_WORDS words of both strings per step, one dependent round
+		 * trip per 8 * DSB_MEM_WORDS bytes instead of per 8 (the bytes past `max` are ignored) */
+		const int W = DSB_MEM_WORDS, NB = 8 * DSB_MEM_WORDS;
+		while (len < max) {
+			uint64_t a[DSB_MEM_WORDS], b[DSB_MEM_WORDS];
+			if (forward) {
+				dsb_ldwu<DSB_MEM_WORDS>(q + len, a);
+				dsb_ldwu<DSB_MEM_WORDS>(t + len, b);
+				for (int k = 0; k < W; k++) {
+					uint64_t x = a[k] ^ b[k];
+					if (x) {
+						len += 8 * k + (__builtin_ctzll(x) >> 3);
+						return DSB_MIN(len, max);
+					}
+				}
+			} else { /* words k = W-1 .. 0 cover the NB bytes ending at q - len; the nearest is k = W-1 */
+				dsb_ldwu<DSB_MEM_WORDS>(q - len - NB + 1, a);
+				dsb_ldwu<DSB_MEM_WORDS>(t - len - NB + 1, b);
+				for (int k = W - 1; k >= 0; k--) {
+					uint64_t x = a[k] ^ b[k];
+					if (x) {
+						len += 8 * (W - 1 - k) + (__builtin_clzll(x) >> 3);
+						return DSB_MIN(len, max);
+					}
+				}
+			}
+			len += NB;
+		}
+		return max > 0 ? max : 0;
+	}
 	if (forward) {
 		while (len < max) {
 			uint64_t x = dsb_ld8u(q + len) ^ dsb_ld8u(t + len);

@@ -270,6 +270,7 @@ struct dsb_gpu_dev {
 	int pin_used[2] = {0, 0};
 	int pin_next = 0;
 	std::vector<dsb_gpu_batch *> spare; /* recycled batches: their device buffers are reused, never freed mid-pipeline */
+	int n_ctx = 1;           /* contexts on this GPU (they split its workspace budget) */
 };
 
 template <typename T>
@@ -293,7 +294,10 @@ extern "C" int dsb_gpu_device_count(void)
 	return n;
 }
 
-static int dev_init(dsb_index *ix, int device, dsb_gpu_dev **out, char *err, size_t errn)
+/* A device context: streams, events, workspace, and the index tables — its own upload, or
+ * those of `share`, an earlier context on the same GPU (several contexts per GPU let batches of
+ * one read_classify call run their kernels side by side, each context with its own workspace). */
+static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu_dev **out, char *err, size_t errn)
 {
 	HIP_OK(hipSetDevice(device));
 	dsb_gpu_dev *g = new dsb_gpu_dev();
@@ -319,6 +323,11 @@ static int dev_init(dsb_index *ix, int device, dsb_gpu_dev **out, char *err, siz
 		for (int ph = 0; ph <= DSB_PH_N; ph++)
 			for (int e = 0; e < 2; e++)
 				HIP_OK(hipEventCreate(&g->pev[k][ph][e]));
+	if (share) { /* read-only tables: one copy per GPU */
+		g->h = share->h;
+		g->d = share->d;
+		return 0;
+	}
 	dsb_dindex_t &h = g->h;
 	memset(&h, 0, sizeof(h));
 	/* occ lines (128 B per 256 BWT symbols, re-laid out by the loader) + one zero line */
@@ -407,9 +416,25 @@ extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
 			snprintf(err, errn, "device %d out of range (%d visible)", devs[k], ndev);
 			return -1;
 		}
+	/* DSB_GPU_CONTEXTS (default 1): contexts per listed GPU, sharing its copy of the index */
+	int per = 1;
+	if (const char *e = getenv("DSB_GPU_CONTEXTS"))
+		per = DSB_MAX(1, DSB_MIN(8, atoi(e)));
+	if (per > 1) {
+		int m = 0, d2[DSB_MAX_GPUS];
+		for (int k = 0; k < n; k++)
+			for (int c = 0; c < per && m < DSB_MAX_GPUS; c++)
+				d2[m++] = devs[k];
+		memcpy(devs, d2, sizeof(int) * m);
+		n = m;
+	}
 	for (int k = 0; k < n; k++) {
 		dsb_gpu_dev *g = nullptr;
-		if (dev_init(ix, devs[k], &g, err, errn)) {
+		const dsb_gpu_dev *share = nullptr;
+		for (int j = 0; j < k && !share; j++)
+			if (((dsb_gpu_dev *)ix->gpus[j])->device == devs[k])
+				share = (const dsb_gpu_dev *)ix->gpus[j];
+		if (dev_init(ix, devs[k], share, &g, err, errn)) {
 			if (g)
 				dev_free(g);
 			for (int j = 0; j < k; j++)
@@ -423,6 +448,12 @@ extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
 	}
 	ix->n_gpu = n;
 	ix->gpu = ix->gpus[0];
+	for (int k = 0; k < n; k++) {
+		dsb_gpu_dev *g = (dsb_gpu_dev *)ix->gpus[k];
+		g->n_ctx = 0;
+		for (int j = 0; j < n; j++)
+			g->n_ctx += ((dsb_gpu_dev *)ix->gpus[j])->device == g->device;
+	}
 	return 0;
 }
 
@@ -521,7 +552,8 @@ static size_t ws_budget(const dsb_gpu_dev *g)
 	size_t fr = 0, tot = 0;
 	if (hipMemGetInfo(&fr, &tot) != hipSuccess)
 		return (size_t)8 << 30;
-	size_t b = (size_t)((double)(fr + g->ws.cap) * 0.7); /* the rest: overflow re-runs (retry buffer), streams */
+	/* the rest: overflow re-runs (retry buffer), streams; contexts sharing the GPU split it */
+	size_t b = (size_t)((double)(fr + g->ws.cap) * 0.7 / g->n_ctx);
 	size_t cap = (size_t)200 << 30;
 	return b < cap ? b : cap;
 }

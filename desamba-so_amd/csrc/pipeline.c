@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <sys/mman.h>
 #include "dsb_host.h"
 #include "pipeline.h"
 #include "gpu/dsb_gpu.h"
@@ -243,6 +244,15 @@ static void *runner(void *arg)
 }
 
 /* ---------------------------------------------------------------- format */
+/* The output is written once by many threads: ask for transparent huge pages on it, so that
+ * its first touch faults 2 MB at a time instead of 4 KB (a hint; ignored where THP is off). */
+static void out_hugepages(char *p, uint64_t n)
+{
+	uintptr_t a = ((uintptr_t)p + 4095) & ~(uintptr_t)4095, e = ((uintptr_t)p + n) & ~(uintptr_t)4095;
+	if (e > a + (2u << 20))
+		madvise((void *)a, e - a, MADV_HUGEPAGE);
+}
+
 typedef struct {
 	pipe_t *p;
 	pbatch *b;
@@ -308,6 +318,7 @@ static int format_batch(pipe_t *p, pbatch *b)
 		}
 		p->out = q;
 		p->out_m = m;
+		out_hugepages(p->out, p->out_m);
 	}
 	c.off = off;
 	dsb_pool_run(p->pool, n_tasks, copy_task, &c);
@@ -351,6 +362,7 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 		snprintf(err, errn, "out of memory for the output (%lu bytes)", (unsigned long)p->out_m);
 		return -1;
 	}
+	out_hugepages(p->out, p->out_m);
 	pthread_t th[2 * DSB_MAX_GPUS];
 	dev_arg args[DSB_MAX_GPUS];
 	for (int d = 0; d < n_dev; d++) {

@@ -8,7 +8,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out
 export TMPDIR=/tmp
 cd /tmp
-B="$R/bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu --no-stats"
+B="$R/bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu --no-stats --no-dropin"
 [ -z "${ONLY_EXTRA:-}" ] && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_kt" -o kt -- python3 $B > "$OUT/prof_kt.json" 2> "$OUT/prof_kt.err"
 [ -z "${ONLY_EXTRA:-}" ] && timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof_fetch" -o pf -- python3 $B > "$OUT/prof_fetch.json" 2> "$OUT/prof_fetch.err"
 [ -z "${ONLY_EXTRA:-}" ] && timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE -d "$OUT/prof_write" -o pw -- python3 $B > "$OUT/prof_write.json" 2> "$OUT/prof_write.err"

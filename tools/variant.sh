@@ -18,6 +18,6 @@ for p in 0 1 2 3 4 5 6 7 8; do
 	fi
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/lib/var_$NAME.so $B/index_load.o $B/fastq.o $B/sam_out.o \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/lib/var_$NAME.so $B/index_load.o $B/fastq.o $B/sam_out.o $B/pool.o $B/pipeline.o \
 	$B/meta.o $B/abi.o $B/kernels.o $OBJS -Wl,--version-script=$D/exports.map -lz -lm -lpthread
 echo "built $D/lib/var_$NAME.so"
