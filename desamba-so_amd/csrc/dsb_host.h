@@ -101,6 +101,17 @@ dsb_parser *dsb_parser_new(const char *buf, uint64_t len);
 uint64_t dsb_parser_next(dsb_parser *p, dsb_reads_t *out, uint64_t max_reads, uint64_t max_bases);
 void dsb_parser_stats(const dsb_parser *p, uint64_t *n_fast, uint64_t *n_slow);
 void dsb_parser_free(dsb_parser *p);
+/* One kseq_t over resident text (the evaluation tools): kseq_read's return value; the accessors
+ * return its buffers (NULL if never set; stale content kept as the reference keeps it). */
+typedef struct dsb_kseq1 dsb_kseq1;
+dsb_kseq1 *dsb_kseq1_open(const char *buf, uint64_t len);
+int64_t dsb_kseq1_read(dsb_kseq1 *k);
+const char *dsb_kseq1_name(const dsb_kseq1 *k);
+const char *dsb_kseq1_comment(const dsb_kseq1 *k);
+const char *dsb_kseq1_seq(const dsb_kseq1 *k);
+const char *dsb_kseq1_qual(const dsb_kseq1 *k);
+uint64_t dsb_kseq1_seq_l(const dsb_kseq1 *k);
+void dsb_kseq1_close(dsb_kseq1 *k);
 /* read a whole (optionally gzip) file or memory buffer (gzip auto-detected) */
 int dsb_slurp_path(const char *path, char **buf, uint64_t *len);
 int dsb_open_path(const char *path, char **buf, uint64_t *len, uint64_t *unmap_len);

@@ -394,6 +394,44 @@ void dsb_reads_free(dsb_reads_t *r)
 	memset(r, 0, sizeof(*r));
 }
 
+/* ------------------------------------------------------------------ one kseq_t */
+/* A single kseq_t reading resident text record by record (the evaluation tools' loops,
+ * reference src/analysis.c:2439-2678): the strings are the kseq buffers themselves, so a
+ * record without a comment shows the previous record's comment and a FASTA record the previous
+ * quality, as printf("%s") of the reference prints them (NULL: never set). */
+struct dsb_kseq1 {
+	kstream_emu ks;
+	slot_state st;
+	kseq_bufs b;
+	int has_qual;
+};
+
+dsb_kseq1 *dsb_kseq1_open(const char *buf, uint64_t len)
+{
+	dsb_kseq1 *k = calloc(1, sizeof(*k));
+	k->ks.buf = (const unsigned char *)buf;
+	k->ks.len = len;
+	return k;
+}
+
+int64_t dsb_kseq1_read(dsb_kseq1 *k)
+{
+	return kseq_read_emu(&k->ks, &k->st, &k->b, &k->has_qual);
+}
+
+const char *dsb_kseq1_name(const dsb_kseq1 *k) { return k->b.name.s; }
+const char *dsb_kseq1_comment(const dsb_kseq1 *k) { return k->b.comment.s; }
+const char *dsb_kseq1_seq(const dsb_kseq1 *k) { return k->b.seq.s; }
+const char *dsb_kseq1_qual(const dsb_kseq1 *k) { return k->b.qual.s; }
+uint64_t dsb_kseq1_seq_l(const dsb_kseq1 *k) { return k->b.seq.l; }
+
+void dsb_kseq1_close(dsb_kseq1 *k)
+{
+	if (!k) return;
+	free(k->b.name.s); free(k->b.comment.s); free(k->b.seq.s); free(k->b.qual.s);
+	free(k);
+}
+
 /* ------------------------------------------------------------------ input sources */
 static int inflate_all(gzFile gz, char **buf, uint64_t *len, uint64_t hint)
 {

@@ -416,8 +416,10 @@ extern "C" int dsb_gpu_init(dsb_index *ix, int device, char *err, size_t errn)
 			snprintf(err, errn, "device %d out of range (%d visible)", devs[k], ndev);
 			return -1;
 		}
-	/* DSB_GPU_CONTEXTS (default 1): contexts per listed GPU, sharing its copy of the index */
-	int per = 1;
+	/* DSB_GPU_CONTEXTS (default 2): contexts per listed GPU, sharing its copy of the index, so
+	 * that consecutive batches of a read_classify call overlap on the GPU and fill each other's
+	 * phase-kernel tails (the batch API uses the first context only) */
+	int per = 2;
 	if (const char *e = getenv("DSB_GPU_CONTEXTS"))
 		per = DSB_MAX(1, DSB_MIN(8, atoi(e)));
 	if (per > 1) {
@@ -544,7 +546,7 @@ static float ev_ms(dsb_gpu_dev *g)
 
 /* workspace budget for one chunk of reads: most of the HBM left after the index (the
  * workspace already held by this device counts as available) */
-static size_t ws_budget(const dsb_gpu_dev *g)
+static size_t ws_budget(const dsb_gpu_dev *g, int share)
 {
 	const char *e = getenv("DSB_WS_BUDGET_MB");
 	if (e)
@@ -552,8 +554,9 @@ static size_t ws_budget(const dsb_gpu_dev *g)
 	size_t fr = 0, tot = 0;
 	if (hipMemGetInfo(&fr, &tot) != hipSuccess)
 		return (size_t)8 << 30;
-	/* the rest: overflow re-runs (retry buffer), streams; contexts sharing the GPU split it */
-	size_t b = (size_t)((double)(fr + g->ws.cap) * 0.7 / g->n_ctx);
+	/* the rest: overflow re-runs (retry buffer), streams; the contexts of a GPU that run the
+	 * batches of one read_classify call side by side split it (share = their number) */
+	size_t b = (size_t)((double)(fr + g->ws.cap) * 0.7 / share);
 	size_t cap = (size_t)200 << 30;
 	return b < cap ? b : cap;
 }
@@ -874,7 +877,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	std::vector<uint64_t> word_off;
 	dsb_read_out_t *ro = b->ro.data();
 	std::vector<dsb_hit_out_t> &hv = b->hits;
-	size_t budget = ws_budget(g);
+	size_t budget = ws_budget(g, hooks ? g->n_ctx : 1);
 	int carry = *max_read_l;
 	int l_ek = ix->l_ek;
 	for (uint64_t cb = 0; cb < n;) {

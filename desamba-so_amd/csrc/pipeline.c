@@ -350,7 +350,7 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 	p->carry0 = *max_read_l;
 	pthread_mutex_init(&p->mu, NULL);
 	pthread_cond_init(&p->cv, NULL);
-	uint64_t max_reads = env_u64("DSB_PIPE_READS", 50000);
+	uint64_t max_reads = env_u64("DSB_PIPE_READS", 25000);
 	uint64_t max_bases = env_u64("DSB_PIPE_MBP", 400) * 1000000ull;
 	uint64_t depth = env_u64("DSB_PIPE_DEPTH", 2 + 2 * (uint64_t)n_dev);
 	if (max_reads == 0) max_reads = 1;
@@ -381,7 +381,9 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 			pthread_mutex_unlock(&p->mu);
 			double tp = now_ms();
 			pbatch *b = calloc(1, sizeof(pbatch));
-			uint64_t got = dsb_parser_next(ps, &b->reads, max_reads, max_bases);
+			/* the first batch is a quarter size, so the GPU starts sooner */
+			uint64_t mr = seq == 0 ? (max_reads + 3) / 4 : max_reads;
+			uint64_t got = dsb_parser_next(ps, &b->reads, mr, max_bases);
 			double dt = now_ms() - tp;
 			pthread_mutex_lock(&p->mu);
 			p->ms_parse += dt;

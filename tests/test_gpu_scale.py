@@ -124,6 +124,7 @@ def test_read_classify_over_two_device_contexts(pyd, fixture_index):
     """DSB_DEVICES=0,0: batches of one read_classify call alternate between two contexts holding
     the index; records and the carried max_read_l equal the single-context call."""
     os.environ["DSB_DEVICES"] = "0,0"
+    os.environ["DSB_GPU_CONTEXTS"] = "1"
     os.environ["DSB_PIPE_READS"] = "41"
     try:
         idx = pyd.Index(fixture_index)
@@ -138,6 +139,21 @@ def test_read_classify_over_two_device_contexts(pyd, fixture_index):
             idx.close()
     finally:
         os.environ.pop("DSB_DEVICES", None)
+        os.environ.pop("DSB_GPU_CONTEXTS", None)
+        os.environ.pop("DSB_PIPE_READS", None)
+
+
+def test_default_two_contexts_share_one_index_copy(gpu_index, pyd):
+    """load_index's default: two contexts on the GPU sharing one copy of the index tables
+    (DSB_GPU_CONTEXTS=2), batches of one call alternating between them."""
+    devs = gpu_index.devices()
+    assert len(devs) == 2 and devs[0] == devs[1]
+    os.environ["DSB_PIPE_READS"] = "64"
+    try:
+        out, t, _ = gpu_index.classify(golden("ont.fq"), fmt=pyd.FMT_SAM)
+        assert out == golden("ont.herm.sam")
+        assert t["n_devices"] == 2 and t["n_batches"] >= 30
+    finally:
         os.environ.pop("DSB_PIPE_READS", None)
 
 
