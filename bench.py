@@ -446,7 +446,7 @@ def main():
         ms_i = per_phase["island"]["avg_launch_ms"]
         per_phase["island"]["achieved_GBs"] = round(ib / (ms_i / 1e3) / 1e9, 3) if ms_i > 0 else None
         d = per_phase[dom]
-        traffic = None
+        traffic = traffic_cal = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tf):
             with open(tf) as f:
@@ -455,8 +455,10 @@ def main():
             tk = re.sub(r"<(\d+)(?:, \d+)*>", r"<\1>", tj.get("kernel") or "")
             if tj.get("workload") == workload and tj.get("reads") == a.reads and tk == KERNEL_OF[dom]:
                 traffic = tj.get("hbm_bytes_per_launch")
+                traffic_cal = tj.get("hbm_bytes_per_launch_calibrated")
         roof = {"bound": "hbm", "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 6), "traffic": traffic, "kernel": KERNEL_OF[dom],
+                "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 6), "traffic": traffic,
+                "traffic_calibrated": traffic_cal, "kernel": KERNEL_OF[dom],
                 "phase": dom, "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
                 "launches_per_step": d["launches_per_step"], "avg_launch_ms": d["avg_launch_ms"], "phases": per_phase}
         stats = {"phases": ts["stats_phase"], "classB": ts["stats_B"]}
@@ -471,6 +473,23 @@ def main():
         if not a.no_dropin:
             full_sha = hashlib.sha256(batch.format(P.FMT_SAM_FULL)).hexdigest()
             dropin = dropin_leg(idx, fq, batch.n_reads, batch.n_bases, full_sha)
+    elif world > 1 and not a.no_dropin:
+        # every rank: one read_classify over its own reads at the same time (after a barrier);
+        # aggregate = all ranks' reads / the slowest rank's call
+        import pydesamba as P
+        full_sha = hashlib.sha256(batch.format(P.FMT_SAM_FULL)).hexdigest()
+        dist.barrier()
+        mine = dropin_leg(idx, fq, batch.n_reads, batch.n_bases, full_sha)
+        t_s = torch.tensor([mine["secs"]], dtype=torch.float64, device=cdev)
+        t_ok = torch.tensor([float(mine["identical_to_batch_records"] is True)], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t_s, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
+        secs, same = float(t_s.item()), bool(t_ok.item())
+        if rank == 0:
+            dropin = {"value": round(batch.n_reads * world / secs, 1), "unit": "reads/s", "secs": round(secs, 4),
+                      "reads": batch.n_reads * world, "ranks": world, "identical_to_batch_records": same,
+                      "rank0": mine,
+                      "what": "every rank: read_classify over its own 100k reads at once; slowest rank's time"}
 
     if rank == 0:
         value = reads_total / elapsed

@@ -2524,6 +2524,9 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 #ifndef DSB_MATCH_PF
 #define DSB_MATCH_PF 0
 #endif
+#ifndef DSB_QR_STATS
+#define DSB_QR_STATS 0
+#endif
 		/* the probe 9-mer of position i = 4m and the window byte it starts at */
 		auto probe = [&](int m, const uint8_t *&cts) -> uint64_t {
 			int i = 4 * m;
@@ -2563,6 +2566,24 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			n_head = heads[n_kmer & KEY_MASK];
 		}
 		if (w->stats && lane == 0) w->stats[DSB_ST_NWIN]++;
+#if DSB_QR_STATS /* dev: read-range histogram of the windows, in delA slots the phase leaves unused */
+		if (w->stats && lane == 0) {
+			int64_t hi = DSB_MIN((int64_t)q_ed, (int64_t)w->L - 9), r = hi - (int64_t)q_bg + 1;
+			uint64_t *s = w->stats;
+			int mid = t_str == w->win + DSB_WIN_MID;
+			if (r < 0) r = 0;
+			r = DSB_MIN(r, (int64_t)1 << 20);
+			if (mid) {
+				s[DSB_ST_OCC]++; s[DSB_ST_OCC_NIB] += r; s[DSB_ST_MEMSEARCH] += n_i;
+				if (r <= 64) { s[DSB_ST_ANCHOR]++; s[DSB_ST_CHAIN] += n_i; }
+				if (r <= 128) { s[DSB_ST_EK1]++; s[DSB_ST_EK2] += n_i; }
+				s[DSB_ST_REPLAY] += t_len;
+			} else {
+				s[DSB_ST_SA]++; s[DSB_ST_UNI] += r; s[DSB_ST_REFPOS] += n_i;
+				if (r <= 1024) s[DSB_ST_PASS2]++;
+			}
+		}
+#endif
 		for (int mb = 0; mb < n_i; mb += DSB_WV) {
 			int m = mb + (int)lane + 1;
 			if (w->stats && lane == 0) w->stats[DSB_ST_NBATCH]++;

@@ -7,8 +7,10 @@
 //             at an address derived from the loaded value, as a hash-list walk does)
 //   k_scatter N random 4-byte stores over a table of T bytes
 //   k_stream  T bytes read once, coalesced (the reference point for the FETCH correction)
+//   k_build   the scoring kernel's read-hash build pattern: each wave owns a table of O KB (a
+//             read's list heads) and each lane does old = t[key]; t[key] = f(old) at random keys
 //
-//   gather_calib <table_MB> <million_accesses>
+//   gather_calib <table_MB> <million_accesses> [own_KB]
 // prints one line per kernel: accesses, HIP-event time; the per-access bytes come from a
 // separate `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` pass over the same command.
 #include <hip/hip_runtime.h>
@@ -59,6 +61,17 @@ __global__ __launch_bounds__(64) void k_scatter(uint32_t *__restrict__ t, uint64
 	}
 }
 
+__global__ __launch_bounds__(64) void k_build(uint32_t *__restrict__ t, uint32_t own_words, uint64_t per_lane)
+{
+	uint64_t id = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+	uint32_t *own = t + (uint64_t)blockIdx.x * own_words;
+	for (uint64_t k = 0; k < per_lane; k++) {
+		uint32_t a = (uint32_t)(mix(id * 0x9E3779B97F4A7C15ull + k + 11) & (own_words - 1));
+		uint32_t old = own[a];
+		own[a] = old + (uint32_t)k;
+	}
+}
+
 __global__ __launch_bounds__(256) void k_stream(const uint4 *__restrict__ t, uint64_t n, uint32_t *__restrict__ sink)
 {
 	uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
@@ -75,6 +88,7 @@ int main(int argc, char **argv)
 {
 	uint64_t mb = argc > 1 ? strtoull(argv[1], 0, 10) : 1024;
 	uint64_t acc_m = argc > 2 ? strtoull(argv[2], 0, 10) : 256;
+	uint64_t own_kb = argc > 3 ? strtoull(argv[3], 0, 10) : 32; /* power of two */
 	uint64_t bytes = mb << 20, words = bytes / 4;
 	uint32_t *t, *sink;
 	CK(hipMalloc(&t, bytes));
@@ -106,6 +120,17 @@ int main(int argc, char **argv)
 	CK(hipEventElapsedTime(&ms, a, b));
 	printf("k_scatter table %lu MB  stores %lu  %.3f ms  %.2f G stores/s\n", (unsigned long)mb,
 	       (unsigned long)(lanes * per_lane), ms, lanes * per_lane / (ms * 1e6));
+
+	uint32_t own_words = (uint32_t)(own_kb * 256);
+	if ((uint64_t)own_words * 4 * (lanes / 64) <= bytes) {
+		CK(hipEventRecord(a));
+		k_build<<<(uint32_t)(lanes / 64), 64>>>(t, own_words, per_lane);
+		CK(hipEventRecord(b));
+		CK(hipEventSynchronize(b));
+		CK(hipEventElapsedTime(&ms, a, b));
+		printf("k_build   own %lu KB per wave  updates %lu  %.3f ms  %.2f G updates/s\n", (unsigned long)own_kb,
+		       (unsigned long)(lanes * per_lane), ms, lanes * per_lane / (ms * 1e6));
+	}
 
 	CK(hipEventRecord(a));
 	k_stream<<<4096, 256>>>((const uint4 *)t, bytes / 16, sink);

@@ -6,7 +6,9 @@ Writes profiles/<tag>/kernel_stats.csv (per-kernel calls / total / average durat
 --kernel-trace --stats pass), profiles/<tag>/pmc.csv (per-kernel average FETCH_SIZE and
 WRITE_SIZE per dispatch, separate passes) and profiles/traffic.json (HBM bytes per launch of
 the dominant kernel: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
-/opt/skills/guides/MI355X_MICROARCH.md §HBM), which bench.py reports as roofline.traffic.
+/opt/skills/guides/MI355X_MICROARCH.md §HBM, which bench.py reports as roofline.traffic; and
+FETCH_SIZE + WRITE_SIZE, the reading tools/gather_calib.hip calibrates for random 4-B accesses,
+reported as roofline.traffic_calibrated).
 """
 import csv
 import json
@@ -66,7 +68,11 @@ def main():
           "avg_duration_ns": int(rows[0][3]),
           "fetch_size_kb_per_launch": round(fs, 1), "write_size_kb_per_launch": round(ws, 1),
           "hbm_bytes_per_launch": int((2 * fs + ws) * 1024),
-          "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of 128-B requests)"}
+          "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of 128-B requests)",
+          # random 4-B gathers report one 64-B unit each (profiles/r03_calib: 49-56 G loads/s would
+          # be 6.3-7.2 TB/s at 128 B, above the 5.8 TB/s streaming rate), scattered stores 32 B
+          "hbm_bytes_per_launch_calibrated": int((fs + ws) * 1024),
+          "calibration": "FETCH_SIZE + WRITE_SIZE: the random-access reading of profiles/r03_calib/calib.json"}
     with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
         json.dump(tj, f, indent=1)
     print(json.dumps(tj, indent=1))
