@@ -269,9 +269,14 @@ DSB_HD int dsb_prev_set3(const uint64_t *ex, int i)
 	return -1;
 }
 
-DSB_HD uint32_t dsb_search_exist(const uint64_t *ex_, uint32_t l_kmer_v, dsb_seed_t *seed_v, uint32_t direction)
+#ifndef DSB_NEED_STATS
+#define DSB_NEED_STATS 0 /* dev: count the exist bits the scan reads (dsb_search_exist's *need) */
+#endif
+DSB_HD uint32_t dsb_search_exist(const uint64_t *ex_, uint32_t l_kmer_v, dsb_seed_t *seed_v, uint32_t direction,
+				 uint64_t *need = nullptr)
 {
 	uint32_t l_seed_v = 0;
+	uint64_t nd = 0;
 	dsb_bitrd_t br = {ex_, 0xffffffffu, 0};
 	dsb_bitrd_t *ex = &br;
 	const uint32_t STEP_EK = 3;
@@ -279,15 +284,19 @@ DSB_HD uint32_t dsb_search_exist(const uint64_t *ex_, uint32_t l_kmer_v, dsb_see
 	 * at a time (dsb_next_set3 / dsb_prev_set3) instead of bit by bit */
 	if (direction == DSB_FORWARD) {
 		for (uint32_t i = STEP_EK - 1; i < l_kmer_v; i += STEP_EK) {
+			uint32_t i0 = i;
 			i = dsb_next_set3(ex_, i, l_kmer_v);
+			if (DSB_NEED_STATS) nd += (DSB_MIN(i, l_kmer_v - 1) - i0) / 3 + 1;
 			if (i >= l_kmer_v)
 				break;
 			uint32_t offset = i, len = 1;
 			for (int j = 1; j < (int)STEP_EK; ++j) {
+				if (DSB_NEED_STATS) nd++;
 				if (dsb_bit(ex, i - j)) { offset--; len++; }
 				else break;
 			}
 			for (int j = 1; i + j < l_kmer_v; ++j) {
+				if (DSB_NEED_STATS) nd++;
 				if (dsb_bit(ex, i + j)) {
 					len++;
 					if (len > 60) break; /* the i += 50 is overwritten below */
@@ -300,15 +309,19 @@ DSB_HD uint32_t dsb_search_exist(const uint64_t *ex_, uint32_t l_kmer_v, dsb_see
 		}
 	} else {
 		for (int i = (int)l_kmer_v - (int)STEP_EK; i >= 0; i -= STEP_EK) {
+			int i0 = i;
 			i = dsb_prev_set3(ex_, i);
+			if (DSB_NEED_STATS) nd += (uint64_t)((i0 - DSB_MAX(i, 0)) / 3 + 1);
 			if (i < 0)
 				break;
 			uint32_t offset = i, len = 1;
 			for (int j = 1; j < (int)STEP_EK; ++j) {
+				if (DSB_NEED_STATS) nd++;
 				if (dsb_bit(ex, (uint32_t)(i + j))) { offset++; len++; }
 				else break;
 			}
 			for (int j = 1; j <= i; ++j) {
+				if (DSB_NEED_STATS) nd++;
 				if (dsb_bit(ex, (uint32_t)(i - j))) {
 					len++;
 					if (len > 60) break;
@@ -320,6 +333,153 @@ DSB_HD uint32_t dsb_search_exist(const uint64_t *ex_, uint32_t l_kmer_v, dsb_see
 			i = (int)(offset - len);
 		}
 	}
+	if (need)
+		*need += nd;
+	return l_seed_v;
+}
+
+/* search_exist_kmer_M2 (src/cly.c:1066-1155) probing the Bloom tables on demand.
+ *
+ * The scan reads the exist bit of only part of the k-mer positions — every 3rd one between
+ * seeds, the neighbours of a hit, the run of hits — so instead of k_seed probing every position
+ * of both strands up front, each scan lane probes what it reads, DSB_LAZY_K positions per batch
+ * (the next grid positions while scanning, the next consecutive positions while extending), all
+ * loads of a batch in flight together.  Bits land in a 64-position window (known / value masks)
+ * that slides with the scan; a bit is always the exact get_exist_kmer result of its position, so
+ * the seeds equal dsb_search_exist's whatever the batch size. */
+#ifndef DSB_LAZY_EXIST
+#define DSB_LAZY_EXIST 0
+#endif
+#ifndef DSB_LAZY_K
+#define DSB_LAZY_K 8
+#endif
+typedef struct {
+	const dsb_dindex_t *ix;
+	const uint8_t *bin; /* the strand's 2-bit bases */
+	int64_t n;          /* k-mer positions */
+	int64_t base;       /* position of window bit 0 */
+	uint64_t known, val;
+	uint64_t p1, p2;    /* first / second table probes issued */
+} dsb_lazy_t;
+
+DSB_HD void dsb_lazy_fill(dsb_lazy_t *z, int64_t p, int step, int cnt)
+{
+	/* the window must hold the whole batch: re-base it around p, keeping bits still inside */
+	int64_t lo = step > 0 ? p - 2 : p + step * (DSB_LAZY_K - 1), hi = step > 0 ? p + step * (DSB_LAZY_K - 1) : p + 2;
+	if (lo < z->base || hi >= z->base + 64) {
+		int64_t nb = step > 0 ? p - 8 : p - 55;
+		int64_t d = nb - z->base;
+		if (d > 0 && d < 64) {
+			z->known >>= d;
+			z->val >>= d;
+		} else if (d < 0 && d > -64) {
+			z->known <<= -d;
+			z->val <<= -d;
+		} else if (d != 0) {
+			z->known = 0;
+			z->val = 0;
+		}
+		z->base = nb;
+	}
+	const dsb_dindex_t *ix = z->ix;
+	uint64_t h[DSB_LAZY_K];
+	uint32_t b[DSB_LAZY_K];
+	int sh[DSB_LAZY_K];
+	bool act[DSB_LAZY_K];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+	for (int d = 0; d < DSB_LAZY_K; d++) { /* first table: every load of the batch issued */
+		int64_t q = p + (int64_t)step * d;
+		sh[d] = (int)(q - z->base);
+		act[d] = d < cnt && q >= 0 && q < z->n && !((z->known >> sh[d]) & 1);
+		uint64_t km = act[d] ? dsb_kmer_at(z->bin + q, ix->l_ek, ix->single_base_max) : 0;
+		h[d] = km;
+		b[d] = 0;
+		if (km) {
+			uint64_t h1 = dsb_hash64_1(km) & ix->ek_mask;
+			b[d] = dsb_gld(ix->ek0 + (h1 >> 3)) >> (7 - (h1 & 7));
+			z->p1++;
+		}
+	}
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+	for (int d = 0; d < DSB_LAZY_K; d++) { /* second table for the first-table hits */
+		uint64_t km = h[d];
+		bool hit = km && (b[d] & 1);
+		b[d] = 0;
+		if (hit) {
+			uint64_t h2 = dsb_hash64_2(km) & ix->ek_mask;
+			b[d] = (dsb_gld(ix->ek1 + (h2 >> 3)) >> (7 - (h2 & 7))) & 1;
+			z->p2++;
+		}
+	}
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+	for (int d = 0; d < DSB_LAZY_K; d++)
+		if (act[d]) {
+			z->known |= 1ull << sh[d];
+			z->val |= (uint64_t)(b[d] & 1) << sh[d];
+		}
+}
+
+DSB_HD int dsb_lazy_bit(dsb_lazy_t *z, int64_t p, int step, int cnt)
+{
+	int64_t o = p - z->base;
+	if (!(o >= 0 && o < 64 && ((z->known >> o) & 1))) {
+		dsb_lazy_fill(z, p, step, cnt);
+		o = p - z->base;
+	}
+	return (int)((z->val >> o) & 1);
+}
+
+DSB_HD uint32_t dsb_search_exist_lazy(dsb_lazy_t *z, uint32_t l_kmer_v, dsb_seed_t *seed_v, uint32_t direction)
+{
+	uint32_t l_seed_v = 0;
+	const int STEP_EK = 3;
+	if (direction == DSB_FORWARD) {
+		for (int64_t i = STEP_EK - 1; i < (int64_t)l_kmer_v; i += STEP_EK) {
+			if (!dsb_lazy_bit(z, i, STEP_EK, DSB_LAZY_K))
+				continue;
+			uint32_t offset = (uint32_t)i, len = 1;
+			for (int j = 1; j < STEP_EK; ++j) {
+				if (dsb_lazy_bit(z, i - j, -1, STEP_EK - j)) { offset--; len++; }
+				else break;
+			}
+			for (int j = 1; i + j < (int64_t)l_kmer_v; ++j) {
+				if (dsb_lazy_bit(z, i + j, 1, DSB_LAZY_K)) {
+					len++;
+					if (len > 60) break; /* the i += 50 is overwritten below */
+				} else break;
+			}
+			seed_v[l_seed_v].offset = offset;
+			seed_v[l_seed_v].len = len;
+			l_seed_v++;
+			i = offset + len;
+		}
+	} else {
+		for (int64_t i = (int64_t)l_kmer_v - STEP_EK; i >= 0; i -= STEP_EK) {
+			if (!dsb_lazy_bit(z, i, -STEP_EK, DSB_LAZY_K))
+				continue;
+			uint32_t offset = (uint32_t)i, len = 1;
+			for (int j = 1; j < STEP_EK; ++j) {
+				if (dsb_lazy_bit(z, i + j, 1, STEP_EK - j)) { offset++; len++; }
+				else break;
+			}
+			for (int j = 1; j <= i; ++j) {
+				if (dsb_lazy_bit(z, i - j, -1, DSB_LAZY_K)) {
+					len++;
+					if (len > 60) break;
+				} else break;
+			}
+			seed_v[l_seed_v].offset = offset - len + 1;
+			seed_v[l_seed_v].len = len;
+			l_seed_v++;
+			i = (int64_t)offset - len;
+		}
+	}
 	return l_seed_v;
 }
 
@@ -328,7 +488,17 @@ DSB_HD void dsb_seed_vector(dsb_read_ws *w, uint32_t strand, uint32_t seed_off, 
 {
 	uint32_t l_kmer_buff = w->L - w->ix->l_ek + 1;
 	dsb_seed_t *seed_v = w->seeds + seed_off;
-	uint32_t l_seed_v = dsb_search_exist(strand ? w->exR : w->exF, l_kmer_buff, seed_v, direction);
+	uint32_t l_seed_v;
+	if (DSB_LAZY_EXIST) {
+		dsb_lazy_t z = {w->ix, w->bin + (strand ? w->L : 0), (int64_t)l_kmer_buff, -(1ll << 40), 0, 0, 0, 0};
+		l_seed_v = dsb_search_exist_lazy(&z, l_kmer_buff, seed_v, direction);
+		if (w->stats) {
+			w->stats[DSB_ST_EK1] += z.p1;
+			w->stats[DSB_ST_EK2] += z.p2;
+		}
+	} else
+		l_seed_v = dsb_search_exist(strand ? w->exR : w->exF, l_kmer_buff, seed_v, direction,
+					    (DSB_NEED_STATS && w->stats) ? w->stats + DSB_ST_OCC : nullptr);
 	uint32_t total_score = 0;
 	int max_index = 0;
 	uint32_t max_length = 0, index_end = 100; /* SEED_RANGE */

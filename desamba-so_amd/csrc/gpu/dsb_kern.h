@@ -122,6 +122,11 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 	w.fast_classify = 1;
 	w.n_hit = 0;
 	w.reached_update = 0;
+	uint64_t st_isl[DSB_ST_N]; /* the scan's own counters: bits read (DSB_NEED_STATS), on-demand probes */
+	if ((DSB_NEED_STATS || DSB_LAZY_EXIST) && STATS == 1) {
+		for (int k = 0; k < DSB_ST_N; k++) st_isl[k] = 0;
+		w.stats = st_isl;
+	}
 	if (L < DSB_MIN_READ_LEN) {
 		f.done = 1;
 	} else {
@@ -153,6 +158,12 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 	}
 	if (strand == 0)
 		dsb_state_save(&w, &f, sp);
+	if ((DSB_NEED_STATS || DSB_LAZY_EXIST) && STATS == 1 && gstats) {
+		const int sl[3] = {DSB_ST_OCC, DSB_ST_EK1, DSB_ST_EK2};
+		for (int k = 0; k < 3; k++)
+			if (st_isl[sl[k]])
+				atomicAdd(gstats + DSB_STATS_SEED + sl[k], (unsigned long long)st_isl[sl[k]]);
+	}
 }
 
 /* One read of a phase of part A with one wavefront per read (dsb_wave.h): fast seeding

@@ -103,6 +103,8 @@ __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ i
 		uint64_t km = dsb_kmer_at(bin + k, l_ek, ix->single_base_max);
 		if (DSB_SEED_PRE)
 			pre[k] = (uint32_t)(km & DSB_PRE_IDX_MASK); /* the seeding's 13-mer prefix (fast / slow J step) */
+		if (DSB_LAZY_EXIST) /* the island scan probes the positions it reads itself */
+			return;
 		if (gstats) { /* work counters: first / second Bloom probes (get_exist_kmer, src/cly.c:951-967) */
 			p1 = km != 0;
 			p2 = p1 && ((dsb_gld(ix->ek0 + ((dsb_hash64_1(km) & ix->ek_mask) >> 3)) >>
@@ -110,6 +112,8 @@ __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ i
 		}
 		e = dsb_exist_kmer(ix, km);
 	}
+	if (DSB_LAZY_EXIST)
+		return;
 	uint64_t bits = __ballot(e);
 	if (lane == 0)
 		ex[word] = bits;
