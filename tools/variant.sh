@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/variant.sh NAME "HIPCC FLAGS" [phases...] — build desamba-so_amd/lib/var_NAME.so: the given
 # phase translation units recompiled with extra flags, linked with the current objects (dev tool
-# for A/B runs on the GPU box: DSB_LIB=desamba-so_amd/lib/var_NAME.so python bench.py ...).
+# for A/B runs; KERNELS=1 also recompiles kernels.hip on the GPU box: DSB_LIB=desamba-so_amd/lib/var_NAME.so python bench.py ...).
 set -euo pipefail
 D=$(cd "$(dirname "$0")/../desamba-so_amd" && pwd)
 NAME=$1; FLAGS=$2; shift 2
@@ -17,7 +17,12 @@ for p in 0 1 2 3 4 5 6 7 8; do
 		OBJS="$OBJS $B/phase$p.o"
 	fi
 done
+KOBJ=$B/kernels.o
+if [ -n "${KERNELS:-}" ]; then # also recompile kernels.hip (k_encode / k_seed / k_classB) with FLAGS
+	/opt/rocm/bin/hipcc $HIPFLAGS $FLAGS -c $D/csrc/gpu/kernels.hip -o $V/kernels.o &
+	KOBJ=$V/kernels.o
+fi
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/lib/var_$NAME.so $B/index_load.o $B/fastq.o $B/sam_out.o $B/pool.o $B/pipeline.o \
-	$B/meta.o $B/abi.o $B/kernels.o $OBJS -Wl,--version-script=$D/exports.map -lz -lm -lpthread
+	$B/meta.o $B/abi.o $KOBJ $OBJS -Wl,--version-script=$D/exports.map -lz -lm -lpthread
 echo "built $D/lib/var_$NAME.so"
