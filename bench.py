@@ -56,7 +56,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 METRIC = "long reads classified/sec + Gbases/sec at 1/2/4/8 MI355X; bit-exact taxid match"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # the phase kernels of classify part A (kernels.hip launch_phase)
-KERNEL_OF = {"island": "k_phase<0>", "fast0": "k_wave_phase<1>", "fast1": "k_wave_phase<2>",
+KERNEL_OF = {"island": "k_island_g<16>", "fast0": "k_wave_phase<1>", "fast1": "k_wave_phase<2>",
              "resolve_f": "k_wave_phase<3>", "slow0": "k_wave_phase<4>", "resolve_s0": "k_wave_phase<5>",
              "slow1": "k_wave_phase<6>", "resolve_s1": "k_wave_phase<7>", "delA": "k_wave_phase<8>"}
 
@@ -428,23 +428,33 @@ def main():
             per_phase[ph] = {"algorithmic_bytes_per_launch": int(b / nl), "avg_launch_ms": round(ms, 3),
                              "launches_per_step": nl,
                              "achieved_GBs": round(b / nl / (ms / 1e3) / 1e9, 3) if ms > 0 else None}
-        # k_seed (the Bloom probes, SURVEY §8d: 1 B per first / second probe) and the island scan
-        # (reads the exist bits k_seed wrote): their counters ride in the island block
+        # the Bloom probes (1 B per first / second probe, what one 1-byte gather costs
+        # is a 64-B sector) ride in the island block: made by k_island_g itself (the default), or
+        # by k_seed over every position before a two-lane island scan of its exist bits
         isl = ts["stats_phase"]["island"]
         probes = isl["ek1"] + isl["ek2"]
-        sb = probes + 2 * batch.n_bases + ts["seed_positions"] // 8  # probes + both strands' bases + exist bits
         ms_seed = sum(t["ms_seed"] for t in tms) / a.steps
-        per_phase["seed"] = {"algorithmic_bytes_per_launch": int(sb), "avg_launch_ms": round(ms_seed, 3),
-                             "launches_per_step": 1,
-                             "achieved_GBs": round(sb / (ms_seed / 1e3) / 1e9, 3) if ms_seed > 0 else None,
-                             "probes": probes, "first_probes": isl["ek1"], "second_probes": isl["ek2"],
-                             "sector_bytes_per_launch": 64 * probes,
-                             "sector_GBs": round(64 * probes / (ms_seed / 1e3) / 1e9, 1) if ms_seed > 0 else None,
-                             "note": "k_seed: one 1-byte Bloom probe costs a 64-B sector; sector_GBs is that rate"}
-        ib = ts["seed_positions"] // 8
-        per_phase["island"]["algorithmic_bytes_per_launch"] = int(ib)
+        probe_info = {"probes": probes, "first_probes": isl["ek1"], "second_probes": isl["ek2"],
+                      "sector_bytes_per_launch": 64 * probes}
+        if ms_seed > 0:
+            sb = probes + 2 * batch.n_bases + ts["seed_positions"] // 8  # probes + both strands' bases + exist bits
+            per_phase["seed"] = dict({"algorithmic_bytes_per_launch": int(sb), "avg_launch_ms": round(ms_seed, 3),
+                                      "launches_per_step": 1,
+                                      "achieved_GBs": round(sb / (ms_seed / 1e3) / 1e9, 3),
+                                      "sector_GBs": round(64 * probes / (ms_seed / 1e3) / 1e9, 1),
+                                      "note": "k_seed: one 1-byte Bloom probe costs a 64-B sector; sector_GBs is that rate"},
+                                     **probe_info)
+            ib = ts["seed_positions"] // 8  # the exist bits the scan reads
+            per_phase["island"]["algorithmic_bytes_per_launch"] = int(ib)
+        else:
+            ib = probes + 2 * batch.n_bases  # the probes + both strands' bases
+            per_phase["island"]["algorithmic_bytes_per_launch"] = int(ib)
+            per_phase["island"].update(probe_info)
         ms_i = per_phase["island"]["avg_launch_ms"]
         per_phase["island"]["achieved_GBs"] = round(ib / (ms_i / 1e3) / 1e9, 3) if ms_i > 0 else None
+        if ms_seed <= 0 and ms_i > 0:
+            per_phase["island"]["sector_GBs"] = round(64 * probes / (ms_i / 1e3) / 1e9, 1)
+            per_phase["island"]["probes_per_s"] = round(probes / (ms_i / 1e3))
         d = per_phase[dom]
         traffic = traffic_cal = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")

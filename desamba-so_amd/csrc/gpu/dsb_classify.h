@@ -338,149 +338,153 @@ DSB_HD uint32_t dsb_search_exist(const uint64_t *ex_, uint32_t l_kmer_v, dsb_see
 	return l_seed_v;
 }
 
-/* search_exist_kmer_M2 (src/cly.c:1066-1155) probing the Bloom tables on demand.
+/* search_exist_kmer_M2 (src/cly.c:1066-1155) in batches of G positions (k_island_g).
  *
- * The scan reads the exist bit of only part of the k-mer positions — every 3rd one between
- * seeds, the neighbours of a hit, the run of hits — so instead of k_seed probing every position
- * of both strands up front, each scan lane probes what it reads, DSB_LAZY_K positions per batch
- * (the next grid positions while scanning, the next consecutive positions while extending), all
- * loads of a batch in flight together.  Bits land in a 64-position window (known / value masks)
- * that slides with the scan; a bit is always the exact get_exist_kmer result of its position, so
- * the seeds equal dsb_search_exist's whatever the batch size. */
-#ifndef DSB_LAZY_EXIST
-#define DSB_LAZY_EXIST 0
+ * The scan reads the exist bit of only part of the k-mer positions (every 3rd one between
+ * seeds, the two neighbours behind a hit, the run of hits after it: 42% of them on C1), so the
+ * island kernel probes the Bloom tables itself instead of k_seed probing every position of both
+ * strands up front.  G lanes scan one strand together: a GRID batch is the next G positions of
+ * the scan's stride-3 grid (i, i+3, ...; backwards i, i-3, ... for the reverse scan), the first
+ * set bit among them is the hit the reference's loop stops at; a RUN1 batch is the hit's two
+ * back neighbours + the first G-2 positions of the run after it; RUN batches continue the run
+ * G positions at a time.  Every batch's bits are probed together (one round trip), the state
+ * update below is the reference loop's over those bits, so the seeds equal dsb_search_exist's
+ * for any G >= 4 (tests/emu/isl_check.cpp replays both over the same bits). */
+#ifndef DSB_ISLAND_G
+#define DSB_ISLAND_G 16 /* lanes per strand (k_island_g); 0: k_seed's exist bits + the two-lane k_island */
 #endif
-#ifndef DSB_LAZY_K
-#define DSB_LAZY_K 8
-#endif
+enum { DSB_ISL_GRID = 0, DSB_ISL_RUN1, DSB_ISL_RUN, DSB_ISL_DONE };
 typedef struct {
-	const dsb_dindex_t *ix;
-	const uint8_t *bin; /* the strand's 2-bit bases */
-	int64_t n;          /* k-mer positions */
-	int64_t base;       /* position of window bit 0 */
-	uint64_t known, val;
-	uint64_t p1, p2;    /* first / second table probes issued */
-} dsb_lazy_t;
+	int32_t mode, i, h, off, ln, p, nk, fwd;
+} dsb_isl_t;
 
-DSB_HD void dsb_lazy_fill(dsb_lazy_t *z, int64_t p, int step, int cnt)
+DSB_HD void dsb_isl_init(dsb_isl_t *s, int nk, int fwd, int live)
 {
-	/* the window must hold the whole batch: re-base it around p, keeping bits still inside */
-	int64_t lo = step > 0 ? p - 2 : p + step * (DSB_LAZY_K - 1), hi = step > 0 ? p + step * (DSB_LAZY_K - 1) : p + 2;
-	if (lo < z->base || hi >= z->base + 64) {
-		int64_t nb = step > 0 ? p - 8 : p - 55;
-		int64_t d = nb - z->base;
-		if (d > 0 && d < 64) {
-			z->known >>= d;
-			z->val >>= d;
-		} else if (d < 0 && d > -64) {
-			z->known <<= -d;
-			z->val <<= -d;
-		} else if (d != 0) {
-			z->known = 0;
-			z->val = 0;
-		}
-		z->base = nb;
-	}
-	const dsb_dindex_t *ix = z->ix;
-	uint64_t h[DSB_LAZY_K];
-	uint32_t b[DSB_LAZY_K];
-	int sh[DSB_LAZY_K];
-	bool act[DSB_LAZY_K];
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
-	for (int d = 0; d < DSB_LAZY_K; d++) { /* first table: every load of the batch issued */
-		int64_t q = p + (int64_t)step * d;
-		sh[d] = (int)(q - z->base);
-		act[d] = d < cnt && q >= 0 && q < z->n && !((z->known >> sh[d]) & 1);
-		uint64_t km = act[d] ? dsb_kmer_at(z->bin + q, ix->l_ek, ix->single_base_max) : 0;
-		h[d] = km;
-		b[d] = 0;
-		if (km) {
-			uint64_t h1 = dsb_hash64_1(km) & ix->ek_mask;
-			b[d] = dsb_gld(ix->ek0 + (h1 >> 3)) >> (7 - (h1 & 7));
-			z->p1++;
-		}
-	}
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
-	for (int d = 0; d < DSB_LAZY_K; d++) { /* second table for the first-table hits */
-		uint64_t km = h[d];
-		bool hit = km && (b[d] & 1);
-		b[d] = 0;
-		if (hit) {
-			uint64_t h2 = dsb_hash64_2(km) & ix->ek_mask;
-			b[d] = (dsb_gld(ix->ek1 + (h2 >> 3)) >> (7 - (h2 & 7))) & 1;
-			z->p2++;
-		}
-	}
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
-	for (int d = 0; d < DSB_LAZY_K; d++)
-		if (act[d]) {
-			z->known |= 1ull << sh[d];
-			z->val |= (uint64_t)(b[d] & 1) << sh[d];
-		}
+	s->nk = nk;
+	s->fwd = fwd;
+	s->i = fwd ? 2 : nk - 3; /* for (i = STEP_EK - 1; ...) / for (i = l_kmer_v - STEP_EK; ...) */
+	s->h = s->off = s->ln = s->p = 0;
+	s->mode = (live && (fwd ? s->i < nk : s->i >= 0)) ? DSB_ISL_GRID : DSB_ISL_DONE;
 }
 
-DSB_HD int dsb_lazy_bit(dsb_lazy_t *z, int64_t p, int step, int cnt)
+/* the position lane gl of the strand's G lanes probes in this batch; -1: none */
+template <int G>
+DSB_HD int dsb_isl_pos(const dsb_isl_t *s, int gl)
 {
-	int64_t o = p - z->base;
-	if (!(o >= 0 && o < 64 && ((z->known >> o) & 1))) {
-		dsb_lazy_fill(z, p, step, cnt);
-		o = p - z->base;
+	int d = s->fwd ? 1 : -1, q;
+	switch (s->mode) {
+	case DSB_ISL_GRID: q = s->i + 3 * d * gl; break;
+	case DSB_ISL_RUN1: q = gl < 2 ? s->h - d * (gl + 1) : s->h + d * (gl - 1); break;
+	case DSB_ISL_RUN: q = s->p + d * gl; break;
+	default: return -1;
 	}
-	return (int)((z->val >> o) & 1);
+	return (q >= 0 && q < s->nk) ? q : -1;
 }
 
-DSB_HD uint32_t dsb_search_exist_lazy(dsb_lazy_t *z, uint32_t l_kmer_v, dsb_seed_t *seed_v, uint32_t direction)
+/* the lowest and highest position the batch probes (lo > hi: none) */
+template <int G>
+DSB_HD void dsb_isl_span(const dsb_isl_t *s, int *lo, int *hi)
 {
-	uint32_t l_seed_v = 0;
-	const int STEP_EK = 3;
-	if (direction == DSB_FORWARD) {
-		for (int64_t i = STEP_EK - 1; i < (int64_t)l_kmer_v; i += STEP_EK) {
-			if (!dsb_lazy_bit(z, i, STEP_EK, DSB_LAZY_K))
-				continue;
-			uint32_t offset = (uint32_t)i, len = 1;
-			for (int j = 1; j < STEP_EK; ++j) {
-				if (dsb_lazy_bit(z, i - j, -1, STEP_EK - j)) { offset--; len++; }
-				else break;
-			}
-			for (int j = 1; i + j < (int64_t)l_kmer_v; ++j) {
-				if (dsb_lazy_bit(z, i + j, 1, DSB_LAZY_K)) {
-					len++;
-					if (len > 60) break; /* the i += 50 is overwritten below */
-				} else break;
-			}
-			seed_v[l_seed_v].offset = offset;
-			seed_v[l_seed_v].len = len;
-			l_seed_v++;
-			i = offset + len;
+	int a = 0, b = -1;
+	if (s->fwd) {
+		switch (s->mode) {
+		case DSB_ISL_GRID: a = s->i; b = s->i + 3 * DSB_MIN(G - 1, (s->nk - 1 - s->i) / 3); break;
+		case DSB_ISL_RUN1: a = s->h - 2; b = DSB_MIN(s->h + G - 2, s->nk - 1); break;
+		case DSB_ISL_RUN: a = s->p; b = DSB_MIN(s->p + G - 1, s->nk - 1); break;
 		}
 	} else {
-		for (int64_t i = (int64_t)l_kmer_v - STEP_EK; i >= 0; i -= STEP_EK) {
-			if (!dsb_lazy_bit(z, i, -STEP_EK, DSB_LAZY_K))
-				continue;
-			uint32_t offset = (uint32_t)i, len = 1;
-			for (int j = 1; j < STEP_EK; ++j) {
-				if (dsb_lazy_bit(z, i + j, 1, STEP_EK - j)) { offset++; len++; }
-				else break;
-			}
-			for (int j = 1; j <= i; ++j) {
-				if (dsb_lazy_bit(z, i - j, -1, DSB_LAZY_K)) {
-					len++;
-					if (len > 60) break;
-				} else break;
-			}
-			seed_v[l_seed_v].offset = offset - len + 1;
-			seed_v[l_seed_v].len = len;
-			l_seed_v++;
-			i = (int64_t)offset - len;
+		switch (s->mode) {
+		case DSB_ISL_GRID: b = s->i; a = s->i - 3 * DSB_MIN(G - 1, s->i / 3); break;
+		case DSB_ISL_RUN1: b = s->h + 2; a = DSB_MAX(s->h - (G - 2), 0); break;
+		case DSB_ISL_RUN: b = s->p; a = DSB_MAX(s->p - (G - 1), 0); break;
 		}
 	}
-	return l_seed_v;
+	*lo = a;
+	*hi = b;
+}
+
+/* one batch: bit g of mb = exist bit of dsb_isl_pos(s, g).  Returns 1 when a seed closes
+ * (*so, *sl = CLY_seed offset / len as search_exist_kmer_M2 stores them). */
+template <int G>
+DSB_HD int dsb_isl_step(dsb_isl_t *s, uint32_t mb, uint32_t *so, uint32_t *sl)
+{
+	int d = s->fwd ? 1 : -1;
+	if (s->mode == DSB_ISL_GRID) {
+		if (mb) { /* the first set grid position: a seed starts there */
+			s->h = s->i + 3 * d * (int)__builtin_ctz(mb);
+			s->off = s->h;
+			s->ln = 1;
+			s->mode = DSB_ISL_RUN1;
+		} else {
+			s->i += 3 * d * G;
+			if (s->fwd ? s->i >= s->nk : s->i < 0)
+				s->mode = DSB_ISL_DONE;
+		}
+		return 0;
+	}
+	if (s->mode != DSB_ISL_RUN1 && s->mode != DSB_ISL_RUN)
+		return 0;
+	int g = 0, cur = s->p, stop = 0;
+	if (s->mode == DSB_ISL_RUN1) { /* for (j = 1; j < STEP_EK; ++j) behind the hit */
+		if (mb & 1) {
+			s->off -= d;
+			s->ln++;
+			if (mb & 2) {
+				s->off -= d;
+				s->ln++;
+			}
+		}
+		g = 2;
+		cur = s->h + d;
+	}
+	for (; g < G; g++, cur += d) { /* the run: i + j < l_kmer_v / j <= i, len > 60 ends it */
+		if (s->fwd ? cur >= s->nk : cur < 0) { stop = 1; break; }
+		if (!((mb >> g) & 1)) { stop = 1; break; }
+		if (++s->ln > 60) { stop = 1; break; }
+	}
+	if (!stop) {
+		s->p = cur;
+		s->mode = DSB_ISL_RUN;
+		return 0;
+	}
+	if (s->fwd) {
+		*so = (uint32_t)s->off;
+		*sl = (uint32_t)s->ln;
+		s->i = s->off + s->ln + 3;
+	} else {
+		*so = (uint32_t)(s->off - s->ln + 1);
+		*sl = (uint32_t)s->ln;
+		s->i = s->off - s->ln - 3;
+	}
+	s->mode = (s->fwd ? s->i < s->nk : s->i >= 0) ? DSB_ISL_GRID : DSB_ISL_DONE;
+	return 1;
+}
+
+/* get_seed_vector_M2's top-seed pass (src/cly.c:1190-1225) over seeds as they are produced: after
+ * seed m is stored with top = 0, the reference writes one more top byte per seed (0 to the
+ * current maximum of the group, or 1 to the maximum of the group seed m closes), and one at the
+ * end; the same writes in the same order leave the same bytes */
+typedef struct { uint32_t n, max_index, max_length, index_end, total; } dsb_topst_t;
+DSB_HD void dsb_top_init(dsb_topst_t *t) { t->n = 0; t->max_index = 0; t->max_length = 0; t->index_end = 100; t->total = 0; }
+/* seed m = t->n with key `key` and length l: *idx gets the seed whose top byte is written, the
+ * return value the byte */
+DSB_HD uint8_t dsb_top_push(dsb_topst_t *t, uint32_t key, uint32_t l, uint32_t *idx)
+{
+	uint32_t m = t->n++;
+	if (key < t->index_end) {
+		if (t->max_length < l) {
+			t->max_length = l;
+			t->max_index = m;
+		}
+		*idx = t->max_index;
+		return 0;
+	}
+	*idx = t->max_index;
+	t->index_end += 100;
+	t->total += t->max_length;
+	t->max_index = m;
+	t->max_length = l;
+	return 1;
 }
 
 /* get_seed_vector_M2, src/cly.c:1157-1229 */
@@ -488,17 +492,8 @@ DSB_HD void dsb_seed_vector(dsb_read_ws *w, uint32_t strand, uint32_t seed_off, 
 {
 	uint32_t l_kmer_buff = w->L - w->ix->l_ek + 1;
 	dsb_seed_t *seed_v = w->seeds + seed_off;
-	uint32_t l_seed_v;
-	if (DSB_LAZY_EXIST) {
-		dsb_lazy_t z = {w->ix, w->bin + (strand ? w->L : 0), (int64_t)l_kmer_buff, -(1ll << 40), 0, 0, 0, 0};
-		l_seed_v = dsb_search_exist_lazy(&z, l_kmer_buff, seed_v, direction);
-		if (w->stats) {
-			w->stats[DSB_ST_EK1] += z.p1;
-			w->stats[DSB_ST_EK2] += z.p2;
-		}
-	} else
-		l_seed_v = dsb_search_exist(strand ? w->exR : w->exF, l_kmer_buff, seed_v, direction,
-					    (DSB_NEED_STATS && w->stats) ? w->stats + DSB_ST_OCC : nullptr);
+	uint32_t l_seed_v = dsb_search_exist(strand ? w->exR : w->exF, l_kmer_buff, seed_v, direction,
+					     (DSB_NEED_STATS && w->stats) ? w->stats + DSB_ST_OCC : nullptr);
 	uint32_t total_score = 0;
 	int max_index = 0;
 	uint32_t max_length = 0, index_end = 100; /* SEED_RANGE */

@@ -129,30 +129,34 @@ DSB_HD uint8_t dsb_cly_bit(uint8_t c)
 	}
 }
 
+/* The l_ek-mer (l <= 24) of the 24 bytes w0 | w1 | w2 (first byte lowest): dsb_kmer_at's value */
+DSB_HD uint64_t dsb_kmer_w(uint64_t wv0, uint64_t wv1, uint64_t wv2, int l, int single_base_max)
+{
+	uint64_t v = 0;
+	uint32_t pc = 0; /* base counts packed 8 bits each */
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+	for (int i = 0; i < 24; i++) {
+		if (i < l) {
+			uint64_t wd = i < 8 ? wv0 : (i < 16 ? wv1 : wv2);
+			uint32_t b = (uint32_t)(wd >> (8 * (i & 7))) & 0xff;
+			v = (v << 2) | b;
+			pc += 1u << (8 * (b & 3));
+		}
+	}
+	uint32_t m = (uint32_t)single_base_max;
+	if ((pc & 0xff) >= m || ((pc >> 8) & 0xff) >= m || ((pc >> 16) & 0xff) >= m || (pc >> 24) >= m)
+		return 0;
+	return v;
+}
+
 /* Rolling l_ek-mer with the low-complexity filter of store_kmers (src/cly.c:359-397):
  * value of bases s[0..l-1] (first base high), 0 when any base count >= single_base_max. */
 DSB_HD uint64_t dsb_kmer_at(const uint8_t *s, int l, int single_base_max)
 {
-	if (l <= 24) { /* three word loads; base counts packed 8 bits each */
-		uint64_t wv0 = dsb_ld8u(s), wv1 = dsb_ld8u(s + 8), wv2 = dsb_ld8u(s + 16);
-		uint64_t v = 0;
-		uint32_t pc = 0;
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
-		for (int i = 0; i < 24; i++) {
-			if (i < l) {
-				uint64_t wd = i < 8 ? wv0 : (i < 16 ? wv1 : wv2);
-				uint32_t b = (uint32_t)(wd >> (8 * (i & 7))) & 0xff;
-				v = (v << 2) | b;
-				pc += 1u << (8 * (b & 3));
-			}
-		}
-		uint32_t m = (uint32_t)single_base_max;
-		if ((pc & 0xff) >= m || ((pc >> 8) & 0xff) >= m || ((pc >> 16) & 0xff) >= m || (pc >> 24) >= m)
-			return 0;
-		return v;
-	}
+	if (l <= 24) /* three word loads */
+		return dsb_kmer_w(dsb_ld8u(s), dsb_ld8u(s + 8), dsb_ld8u(s + 16), l, single_base_max);
 	int cnt[4] = {0, 0, 0, 0};
 	uint64_t v = 0;
 	for (int i = 0; i < l; i++) {

@@ -21,6 +21,9 @@
 #ifndef DSB_MINW_DELA
 #define DSB_MINW_DELA 8
 #endif
+#ifndef DSB_MINW_ISLAND
+#define DSB_MINW_ISLAND 8
+#endif
 #ifndef DSB_MINW_RESOLVE
 #define DSB_MINW_RESOLVE 4
 #endif
@@ -123,7 +126,7 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 	w.n_hit = 0;
 	w.reached_update = 0;
 	uint64_t st_isl[DSB_ST_N]; /* the scan's own counters: bits read (DSB_NEED_STATS), on-demand probes */
-	if ((DSB_NEED_STATS || DSB_LAZY_EXIST) && STATS == 1) {
+	if (DSB_NEED_STATS && STATS == 1) {
 		for (int k = 0; k < DSB_ST_N; k++) st_isl[k] = 0;
 		w.stats = st_isl;
 	}
@@ -158,11 +161,187 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 	}
 	if (strand == 0)
 		dsb_state_save(&w, &f, sp);
-	if ((DSB_NEED_STATS || DSB_LAZY_EXIST) && STATS == 1 && gstats) {
+	if (DSB_NEED_STATS && STATS == 1 && gstats) {
 		const int sl[3] = {DSB_ST_OCC, DSB_ST_EK1, DSB_ST_EK2};
 		for (int k = 0; k < 3; k++)
 			if (st_isl[sl[k]])
 				atomicAdd(gstats + DSB_STATS_SEED + sl[k], (unsigned long long)st_isl[sl[k]]);
+	}
+}
+
+/* The island phase probing the Bloom tables itself (DSB_ISLAND_G lanes per strand, both strands
+ * of a read in one wave; dsb_isl_* in dsb_classify.h): search_exist_kmer_M2 + get_seed_vector_M2
+ * + getIsland (src/cly.c:1066-1263) without k_seed's exist bits.  Each batch, every lane probes
+ * one position (get_exist_kmer, src/cly.c:951-967: the l_ek-mer, table 0, table 1 for a hit),
+ * the strand's G bits come from one ballot, and the strand's lanes update the same scan state.
+ * The lanes also store the 13-mer prefix value (the seeding J step's) of the positions that can
+ * lie inside a seed: every run batch position and each grid hit.  H8: when the forward list runs
+ * past L/4 the reverse strand redoes its scan after the forward stores, so its values win
+ * there, and the read's prefix values are then filled for every position. */
+#ifndef DSB_ISL_WIN
+#define DSB_ISL_WIN 1
+#endif
+template <int G, int STATS>
+__global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+								   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+								   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+								   dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
+								   unsigned long long *__restrict__ gstats, uint32_t dbg, uint32_t tag)
+{
+	static_assert(G >= 4 && G <= 32 && (G & (G - 1)) == 0, "lanes per strand: 4, 8, 16 or 32");
+	(void)dbg; (void)ro; (void)n_overflow; (void)tag;
+	const uint32_t GM = G == 32 ? 0xffffffffu : ((1u << G) - 1);
+	uint32_t lane = threadIdx.x, sg = lane / G, gl = lane % G;
+	uint32_t t = blockIdx.x * (64 / (2 * G)) + (sg >> 1), strand = sg & 1;
+	int live = t < n;
+	uint32_t r = live ? order[t] : 0;
+	uint32_t L = live ? len[r] : 0;
+	int l_ek = ix->l_ek, sbm = ix->single_base_max;
+	uint8_t *base = ws + (live ? ws_off[r] : 0);
+	int run = live && L >= DSB_MIN_READ_LEN;
+	int nk = run ? (int)L - l_ek + 1 : 0; /* l_kmer_buff */
+	/* the read's buffers (dsb_ws_init's carving, without the rest of the per-read state) */
+	dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, live ? scale[r] : DSB_SCALE_UNIT));
+	uint64_t sb = lay.bin + DSB_BIN_GUARD + strand * L; /* the strand's first base */
+	uint32_t *pre = (uint32_t *)(base + lay.pre) + strand * L;
+	dsb_seed_t *seed_v = (dsb_seed_t *)(base + lay.seeds) + (strand ? L >> 2 : 0);
+	dsb_rstate_t *sp = (dsb_rstate_t *)(base + lay.state);
+	uint32_t p1 = 0, p2 = 0;
+	dsb_topst_t top;
+	dsb_top_init(&top);
+	uint32_t l_fwd = 0;
+#if DSB_ISL_WIN
+	/* the strand as aligned 8-byte words: position q is byte (q + bo) of word 0 (the workspace
+	 * base is 8-aligned; the window never starts before it) */
+	const uint64_t *bw = (const uint64_t *)(base + (sb & ~7ull));
+	int bo = (int)(sb & 7);
+	int64_t wmin = -(int64_t)(sb >> 3), wb = INT64_MIN / 2;
+	uint64_t wv = 0;
+#else
+	const uint8_t *bin = base + sb;
+#endif
+	for (int pass = 0; pass < 2; pass++) {
+		/* pass 1: only the reverse strands of reads whose forward list reached L/4 */
+		int mine = run && (pass == 0 || (strand == 1 && l_fwd > (L >> 2)));
+		if (!__ballot(mine))
+			break;
+		dsb_isl_t s;
+		dsb_isl_init(&s, nk, strand == 0, mine);
+		if (mine)
+			dsb_top_init(&top);
+		for (;;) {
+			if (!__ballot(s.mode != DSB_ISL_DONE))
+				break;
+			int q = dsb_isl_pos<G>(&s, (int)gl);
+			int b = 0;
+			uint32_t pv = 0;
+#if DSB_ISL_WIN
+			/* the bytes of the batch's k-mers as aligned words of the strand: lane gl of the
+			 * group holds word wb + gl of a G-word window, reloaded (one coalesced load) only
+			 * when the batch leaves it; each k-mer's four words come by lane shuffles */
+			int lo, hi;
+			dsb_isl_span<G>(&s, &lo, &hi);
+			int64_t klo = ((int64_t)lo + bo) >> 3, khi = (((int64_t)hi + bo) >> 3) + 3;
+			if (s.mode != DSB_ISL_DONE && lo <= hi && (klo < wb || khi >= wb + G)) {
+				wb = s.fwd ? klo : DSB_MAX(khi - (G - 1), wmin);
+				wv = dsb_gld(bw + wb + gl);
+			}
+			int src = q >= 0 ? (int)(sg * G) + (int)((((int64_t)q + bo) >> 3) - wb) : (int)lane;
+			uint64_t wq[4];
+#pragma unroll
+			for (int j = 0; j < 4; j++) {
+				int sj = q >= 0 ? src + j : (int)lane;
+				wq[j] = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(wv >> 32), sj) << 32) |
+					(uint32_t)__shfl((int)(uint32_t)wv, sj);
+			}
+			if (q >= 0) {
+				uint32_t sh = (uint32_t)((q + bo) & 7) * 8;
+				uint64_t x0 = sh ? (wq[0] >> sh) | (wq[1] << (64 - sh)) : wq[0];
+				uint64_t x1 = sh ? (wq[1] >> sh) | (wq[2] << (64 - sh)) : wq[1];
+				uint64_t x2 = sh ? (wq[2] >> sh) | (wq[3] << (64 - sh)) : wq[2];
+				uint64_t km = dsb_kmer_w(x0, x1, x2, l_ek, sbm);
+#else
+			if (q >= 0) {
+				uint64_t km = dsb_kmer_at(bin + q, l_ek, sbm);
+#endif
+				pv = (uint32_t)(km & DSB_PRE_IDX_MASK);
+				if (km) {
+					uint64_t h1 = dsb_hash64_1(km) & ix->ek_mask;
+					p1++;
+					if ((dsb_gld(ix->ek0 + (h1 >> 3)) >> (7 - (h1 & 0x7))) & 0x1) {
+						uint64_t h2 = dsb_hash64_2(km) & ix->ek_mask;
+						p2++;
+						b = (dsb_gld(ix->ek1 + (h2 >> 3)) >> (7 - (h2 & 0x7))) & 0x1;
+					}
+				}
+			}
+			uint32_t mb = (uint32_t)(__ballot(b) >> (sg * G)) & GM;
+			if (q >= 0 && (s.mode != DSB_ISL_GRID || (mb && (int)gl == __builtin_ctz(mb))))
+				pre[q] = pv;
+			uint32_t so = 0, sl = 0;
+			if (dsb_isl_step<G>(&s, mb, &so, &sl) && gl == 0) {
+				uint32_t m = top.n, ti;
+				seed_v[m].offset = so;
+				seed_v[m].len = sl;
+				seed_v[m].top = 0;
+				uint8_t tv = dsb_top_push(&top, strand == 0 ? so : (uint32_t)nk - so - sl, sl, &ti);
+				seed_v[ti].top = tv;
+			}
+		}
+		if (mine && gl == 0) {
+			seed_v[top.max_index].top = 1; /* also when no seed (a stale slot, as the reference) */
+			top.total += top.max_length;
+		}
+		/* the forward lists' lengths, then (pass 1) the reverse pass after the forward stores */
+		uint32_t lf = (uint32_t)__shfl((int)top.n, (int)(lane & ~(2u * G - 1)));
+		if (pass == 0)
+			l_fwd = lf;
+		__threadfence_block();
+	}
+	/* H8: a reverse list rewritten over the forward one moves the seeds the J step starts from:
+	 * store the prefix value of every position of both strands of such a read */
+	if (__ballot(run && l_fwd > (L >> 2))) {
+		if (run && l_fwd > (L >> 2))
+			for (int q = (int)gl; q < nk; q += G)
+				pre[q] = (uint32_t)(dsb_kmer_at(base + sb + q, l_ek, sbm) & DSB_PRE_IDX_MASK);
+	}
+	/* getIsland's SEARCH_DIRs + the read's state for the next phases (k_island's, dsb_phase
+	 * ISLAND): the forward group's lane 0 takes the reverse group's results */
+	uint32_t rn = (uint32_t)__shfl((int)top.n, (int)(lane + G) & 63);
+	uint32_t rt = (uint32_t)__shfl((int)top.total, (int)(lane + G) & 63);
+	if (live && strand == 0 && gl == 0) {
+		dsb_rflags_t f = {0, 0, 0, 0};
+		dsb_sdir_t a = {0, top.n, 0, DSB_FORWARD, top.total}, c = {L >> 2, rn, 1, DSB_REVERSE, rt};
+		if (L < DSB_MIN_READ_LEN) {
+			f.done = 1;
+			a = sp->sd[0]; /* untouched, as k_island leaves them */
+			c = sp->sd[1];
+		} else {
+			if (a.total_score < c.total_score) {
+				dsb_sdir_t x = a;
+				a = c;
+				c = x;
+			}
+			f.both = ((a.total_score - c.total_score) <= (a.total_score >> 3));
+		}
+		sp->sd[0] = a;
+		sp->sd[1] = c;
+		sp->n_anc = 0;
+		sp->n_hit = 0;
+		sp->fast_classify = 1;
+		sp->overflow = 0;
+		sp->reached_update = 0;
+		sp->f = f;
+	}
+	if (STATS == 1 && gstats) {
+		for (int o = 32; o >= 1; o >>= 1) {
+			p1 += (uint32_t)__shfl_xor((int)p1, o);
+			p2 += (uint32_t)__shfl_xor((int)p2, o);
+		}
+		if (lane == 0) {
+			atomicAdd(gstats + DSB_STATS_SEED + DSB_ST_EK1, (unsigned long long)p1);
+			atomicAdd(gstats + DSB_STATS_SEED + DSB_ST_EK2, (unsigned long long)p2);
+		}
 	}
 }
 

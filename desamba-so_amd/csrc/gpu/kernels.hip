@@ -103,8 +103,6 @@ __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ i
 		uint64_t km = dsb_kmer_at(bin + k, l_ek, ix->single_base_max);
 		if (DSB_SEED_PRE)
 			pre[k] = (uint32_t)(km & DSB_PRE_IDX_MASK); /* the seeding's 13-mer prefix (fast / slow J step) */
-		if (DSB_LAZY_EXIST) /* the island scan probes the positions it reads itself */
-			return;
 		if (gstats) { /* work counters: first / second Bloom probes (get_exist_kmer, src/cly.c:951-967) */
 			p1 = km != 0;
 			p2 = p1 && ((dsb_gld(ix->ek0 + ((dsb_hash64_1(km) & ix->ek_mask) >> 3)) >>
@@ -112,8 +110,6 @@ __global__ __launch_bounds__(256) void k_seed(const dsb_dindex_t *__restrict__ i
 		}
 		e = dsb_exist_kmer(ix, km);
 	}
-	if (DSB_LAZY_EXIST)
-		return;
 	uint64_t bits = __ballot(e);
 	if (lane == 0)
 		ex[word] = bits;
@@ -633,7 +629,7 @@ static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, 
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
 				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), dbg, tag);
 	else
-		hipLaunchKernelGGL(fn, dim3(((ph == DSB_PH_ISLAND ? 2 : 1) * m + 63) / 64), dim3(64), 0, s, g->d, cl, g->ws_off.as<uint64_t>(),
+		hipLaunchKernelGGL(fn, dim3(((ph == DSB_PH_ISLAND ? 2 * DSB_MAX(1, DSB_ISLAND_G) : 1) * m + 63) / 64), dim3(64), 0, s, g->d, cl, g->ws_off.as<uint64_t>(),
 				   g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(), g->cnt.as<uint32_t>(),
 				   g->stats.as<unsigned long long>(), dbg, tag);
 }
@@ -746,7 +742,7 @@ static int split_seed(void)
 {
 	static int v = -1;
 	if (v < 0)
-		v = getenv("DSB_NO_SPLIT_SEED") ? 0 : 1;
+		v = (DSB_ISLAND_G > 0 || getenv("DSB_NO_SPLIT_SEED")) ? 0 : 1; /* k_island_g: no k_seed to overlap */
 	return v;
 }
 
@@ -1011,7 +1007,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			HIP_OK(hipMemcpyAsync(g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
 			T.n_launch_phase += 1;
 		}
-		if (tw) {
+		if (tw && DSB_ISLAND_G == 0) {
 			hipEventRecord(g->ev_a, s);
 			k_seed<<<(uint32_t)((tw * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
 										     g->word_off.as<uint64_t>(), nullptr, cn, tw, sst);
@@ -1099,7 +1095,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				return -1;
 			}
 			k_encode<<<m, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, g->sel.as<uint32_t>(), m);
-			if (tw2)
+			if (tw2 && DSB_ISLAND_G == 0)
 				k_seed<<<(uint32_t)((tw2 * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
 											      g->wo2.as<uint64_t>(), g->sel.as<uint32_t>(), m, tw2, nullptr);
 			HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));

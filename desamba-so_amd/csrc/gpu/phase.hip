@@ -4,7 +4,7 @@
  * and each gets its own register allocation.  kernels.hip obtains the kernel through
  * dsb_phase_kernel_<n>(wave, stats).
  *
- * Phase 0 (island scan) runs one lane per read; phases 1-8 run one wavefront per read.  The
+ * Phase 0 (island scan) runs 2 x DSB_ISLAND_G lanes per read (k_island_g); phases 1-8 run one wavefront per read.  The
  * lane-per-read variants of phases 1-8 are diagnostics only (DSB_WAVE_PHASES) and are
  * compiled in with -DDSB_LANE_PHASES=1.
  */
@@ -22,8 +22,12 @@
 extern "C" dsb_phase_fn DSB_CAT(dsb_phase_kernel_, DSB_PH)(int wave, int stats)
 {
 #if DSB_PH == 0
-	(void)wave; /* two lanes per read (k_island); launched with 2 x reads threads */
+	(void)wave;
+#if DSB_ISLAND_G > 0 /* 2 x DSB_ISLAND_G lanes per read, probing the Bloom tables itself */
+	return stats == 1 ? k_island_g<DSB_ISLAND_G, 1> : k_island_g<DSB_ISLAND_G, 0>;
+#else /* two lanes per read over k_seed's exist bits; launched with 2 x reads threads */
 	return stats == 1 ? k_island<1> : (stats == 2 ? k_island<2> : k_island<0>);
+#endif
 #else
 	if (wave)
 		return stats == 1 ? k_wave_phase<DSB_PH, 1> : (stats == 2 ? k_wave_phase<DSB_PH, 2> : k_wave_phase<DSB_PH, 0>);
