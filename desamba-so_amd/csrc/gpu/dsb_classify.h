@@ -106,6 +106,7 @@ typedef struct {
 	dsb_spd_t *sms_lds;     /* wave scoring: the first DSB_SMS_LDS sms entries live in LDS */
 	uint64_t *lds_key;      /* wave chaining: anchor sort keys / ids in LDS (DSB_SORT_LDS entries), or 0 */
 	uint32_t *lds_id;
+	uint16_t *lds_cand;     /* wave scoring: 64 candidate slots of the register k-mer match (DSB_MATCH_BF), or 0 */
 	uint8_t *lds_hb;        /* wave read-hash build: DSB_HB_LDS lane-id bytes in LDS (key groups of a chunk), or 0 */
 	uint32_t *hh[2], *hn[2]; /* read 9-mer hash per strand: list heads per key, one node per position */
 	dsb_sch_t *sch;         /* 256 + 2*400 */
@@ -2721,6 +2722,102 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			}
 			return kmer;
 		};
+#ifndef DSB_MATCH_BF
+#define DSB_MATCH_BF 0 /* measured: 3 -> scoring 56.7 -> 60.6 ms, 2 -> 59.2 ms (the compare loop and its spills cost more than the head loads): off */
+#endif
+		/* Forward windows whose read range [q_bg, q_ed] is at most 64 x DSB_MATCH_BF positions
+		 * (most sdp_middle windows): the candidates of a probe are the range's positions whose
+		 * read 9-mer equals the probe's — exactly the list entries the lookup keeps (key and
+		 * high bits equal, position in the range, in increasing position order) — so they are
+		 * found by comparing the probes with the range's 9-mers held in registers (3 per lane)
+		 * instead of head / node loads from the read hash.  Candidates go to 64 LDS slots in
+		 * (probe, position) order and are extended one per lane; accepted matches are appended
+		 * in that order, as the reference's loop appends them. */
+#if DSB_MATCH_BF
+		if (isForward && w->lds_cand && w->L >= DSB_S_A_KMER_L) {
+			uint32_t qhi = DSB_MIN(q_ed, w->L - DSB_S_A_KMER_L); /* the hash holds positions < L - 8 */
+			uint32_t nr = q_bg <= qhi ? qhi - q_bg + 1 : 0;
+			if (nr <= (uint32_t)(DSB_WV * DSB_MATCH_BF)) {
+				if (w->stats && lane == 0) { w->stats[DSB_ST_NWIN]++; w->stats[DSB_ST_NBATCH] += (n_i + DSB_WV - 1) / DSB_WV; }
+				if (nr == 0)
+					return;
+				uint32_t rk[DSB_MATCH_BF];
+				for (int j = 0; j < DSB_MATCH_BF; j++) {
+					uint32_t qq = lane + (uint32_t)(DSB_WV * j);
+					rk[j] = qq < nr ? dsb_q9mer(q_str + q_bg + qq) : 0xffffffffu;
+				}
+				uint16_t *cl = w->lds_cand;
+				for (int mb = 0; mb < n_i; mb += DSB_WV) {
+					int np = DSB_MIN(DSB_WV, n_i - mb);
+					const uint8_t *pc_t = t_str;
+					uint32_t pk = (int)lane < np ? (uint32_t)probe(mb + (int)lane + 1, pc_t) : 0xfffffffeu;
+					uint32_t nc = 0; /* candidates in the slots (uniform) */
+					/* extend the slotted candidates, one per lane, and append the matches in order */
+					auto flush = [&]() {
+						dsb_wsync();
+						uint32_t ok = 0;
+						dsb_spd_t e = {0, 0, 0, 0};
+						if (lane < nc) {
+							uint32_t c = cl[lane];
+							int m = mb + (int)(c >> 10) + 1, i = 4 * m;
+							uint32_t q_pos = q_bg + (c & 1023u);
+							const uint8_t *c_t_str = t_str + i;
+							if (w->stats) w->stats[DSB_ST_NCAND]++;
+							int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, 4);
+							if (back_len < 4 || i == 4) {
+								uint32_t max_search = q_ed - q_pos - 1;
+								max_search = DSB_MIN(max_search, t_len - i - 1) + DSB_OVER_SEARCH;
+								int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L,
+												 1, (int)max_search);
+								int total_len = back_len + forward_len + 1;
+								if (total_len >= 4) {
+									e.len = total_len;
+									e.q_pos = q_pos - back_len;
+									e.t_pos = i - back_len + t_st;
+									ok = 1;
+								}
+							}
+						}
+						uint32_t tot, off = dsb_wscan(ok, &tot);
+						if (tot) {
+							if (w->n_sms + tot > w->cap.sms) {
+								w->overflow |= 16;
+							} else {
+								if (ok) { dsb_spd_t *d = dsb_sms(w, w->n_sms + off); d->len = e.len; d->q_pos = e.q_pos; d->t_pos = e.t_pos; }
+								w->n_sms += tot;
+							}
+						}
+						nc = 0;
+						dsb_wsync();
+					};
+					for (int p = 0; p < np; p++) {
+						uint32_t pkp = (uint32_t)dsb_wshfl((int)pk, p);
+						for (int j = 0; j < DSB_MATCH_BF; j++) {
+							uint64_t mk = dsb_wballot(rk[j] == pkp);
+							if (!mk)
+								continue;
+							uint32_t cnt = (uint32_t)__builtin_popcountll(mk);
+							if (nc + cnt > (uint32_t)DSB_WV) {
+								flush();
+								if (w->overflow) return;
+							}
+							if ((mk >> lane) & 1) {
+								uint64_t below = lane == 0 ? 0 : (mk & (~0ull >> (64 - lane)));
+								cl[nc + (uint32_t)__builtin_popcountll(below)] = (uint16_t)(((uint32_t)p << 10) | (lane + (uint32_t)(DSB_WV * j)));
+							}
+							nc += cnt;
+						}
+					}
+					if (nc) {
+						flush();
+						if (w->overflow) return;
+					}
+				}
+				dsb_wsync();
+				return;
+			}
+		}
+#endif
 		/* software pipeline: the next batch's probe and list head are loaded before this
 		 * batch's lists are walked, so that their latency overlaps the walk */
 		const uint8_t *n_cts = t_str;

@@ -43,6 +43,7 @@
 #define DSB_TL 0
 #endif
 #define DSB_DELA_LDS_BYTES (DSB_WIN_LDS_BYTES + 64 > DSB_HB_LDS ? DSB_WIN_LDS_BYTES + 64 : DSB_HB_LDS)
+#define DSB_DELA_CAND_OFF 3840 /* 64 u16 candidate slots (dsb_sdp_match_impl, DSB_MATCH_BF) */
 static_assert(sizeof(dsb_rstate_t) <= DSB_STATE_BYTES, "per-read phase state must fit its workspace slot");
 
 /* One phase of classify part A (dsb_phase), one lane per read; the read's control state
@@ -400,6 +401,10 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 			w.lds_hb = (uint8_t *)dela_lds;
 			if (DSB_WIN_IN_LDS)
 				w.win = (uint8_t *)dela_lds;
+			/* the register k-mer match's candidate slots: past the windows, inside the build's area */
+			static_assert(DSB_WIN_LDS_BYTES <= DSB_DELA_CAND_OFF && DSB_DELA_CAND_OFF + 128 <= DSB_DELA_LDS_BYTES,
+				      "candidate slots must not overlap the windows");
+			w.lds_cand = (uint16_t *)((uint8_t *)dela_lds + DSB_DELA_CAND_OFF);
 			dsb_phase<true>(&w, &f, ph);
 		} else
 			dsb_phase<true>(&w, &f, ph);

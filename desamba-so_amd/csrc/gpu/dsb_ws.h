@@ -100,6 +100,7 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 	w->lds_key = 0;
 	w->lds_id = 0;
 	w->lds_hb = 0;
+	w->lds_cand = 0;
 	uint32_t *h = (uint32_t *)(base + o.hash);
 	uint64_t hs = 1ull << o.kl;
 	for (int s = 0; s < 2; s++) {

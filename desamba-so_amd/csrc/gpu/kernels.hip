@@ -22,6 +22,7 @@
 #include <string.h>
 #include <time.h>
 #include <vector>
+#include <atomic>
 #include <algorithm>
 #include "dsb_ws.h"
 #include "dsb_gpu.h"
@@ -259,7 +260,7 @@ struct dsb_gpu_dev {
 	dsb_dindex_t *d;         /* device copy */
 	std::vector<void *> allocs;
 	dbuf ws_off, scale, ws, wsr, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2, woA, woB;
-	uint32_t tag = 0;        /* phase-launch counter: the seeding sp_set slot tags (dsb_hset_tag) */
+	uint32_t tag = 0;        /* tag of this context's last phase launch (dsb_hset_tag; next_launch_tag) */
 	/* streamed batches (read_classify pipeline): uploads on their own stream through pinned
 	 * staging, under their own lock, beside the kernels of the batch before */
 	hipStream_t cstream;
@@ -599,6 +600,13 @@ static uint32_t wave_phases(void)
 	       (1u << DSB_PH_RESOLVE_S0) | (1u << DSB_PH_SLOW1) | (1u << DSB_PH_RESOLVE_S1) | (1u << DSB_PH_DELA);
 }
 
+/* Seeding sp_set slots carry the tag of the launch that wrote them (dsb_hset_tag) and are never
+ * cleared, so a tag must never repeat on workspace bytes: one counter for the whole process
+ * (every context of every GPU: a context's workspace may be re-allocated over bytes another
+ * context wrote), and workspace buffers are zero-filled when allocated (tag 0 is never used). */
+static std::atomic<uint32_t> g_launch_tag{0};
+static uint32_t next_launch_tag(void) { return ++g_launch_tag; }
+
 /* one phase of part A over the reads order[0..m) */
 static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, uint8_t *wsb, const uint32_t *order,
 			 uint32_t m, hipStream_t s = 0)
@@ -614,9 +622,9 @@ static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, 
 	uint32_t dbg = wave_dbg();
 	/* every launch gets its own slot tag; if the 32-bit counter ever wraps, the workspace is
 	 * cleared once (both streams drained) so that no slot of an earlier launch can match */
-	if (++g->tag == 0) {
+	if ((g->tag = next_launch_tag()) == 0) {
 		hipDeviceSynchronize();
-		g->tag = 1;
+		g->tag = next_launch_tag();
 		if (g->ws.p)
 			hipMemsetAsync(g->ws.p, 0, g->ws.cap, s);
 		if (g->wsr.p) /* the retry buffer holds tagged sp_set slots too */
@@ -894,9 +902,12 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		uint32_t cn = (uint32_t)(ce - cb);
 		T.n_chunks++;
 		uint64_t rused = 0; /* bytes of the retry buffer holding this chunk's re-run reads */
+		void *ws_before = g->ws.p;
 		if (g->ws.ensure(ws_total + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
 		    g->word_off.ensure(8 * (size_t)cn + 16, err, errn))
 			return -1;
+		if (g->ws.p != ws_before) /* fresh bytes: no stale sp_set slot may carry a live tag */
+			HIP_OK(hipMemsetAsync(g->ws.p, 0, g->ws.cap, s));
 		HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
 		HIP_OK(hipMemcpyAsync(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
 		const uint32_t *cl = b->d_len.as<uint32_t>() + cb;
@@ -1063,6 +1074,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				void *np = nullptr;
 				size_t need = rused + tot2 + (rused + tot2) / 2 + 4096;
 				HIP_OK(hipMalloc(&np, need));
+				HIP_OK(hipMemsetAsync(np, 0, need, s));
 				if (rused)
 					HIP_OK(hipMemcpyAsync(np, g->wsr.p, rused, hipMemcpyDeviceToDevice, s));
 				HIP_OK(hipStreamSynchronize(s));

@@ -65,8 +65,10 @@ def exist_bits(codes, l, sbm, ek0, ek1, mask):
     return ((v != 0) & (b1 == 1) & (b2 == 1)).astype(np.uint8)
 
 
-def scan_fwd(bits, G):
-    """forward scan with G-position batches; returns (probes, batches, needed, seeds)"""
+def scan_fwd(bits, G, GR=None):
+    """forward scan with G-position grid batches and GR-position run batches; returns
+    (probes, batches, needed, seeds)"""
+    GR = GR or G
     n = len(bits)
     probes = batches = 0
     need = set()
@@ -92,7 +94,7 @@ def scan_fwd(bits, G):
         # first run batch: h-1, h-2, h+1 .. h+G-2
         back = [h - 1, h - 2]
         fwd0 = h + 1
-        nf = G - 2
+        nf = GR - 2
         probes += 2
         batches += 1
         for p in back:
@@ -122,7 +124,7 @@ def scan_fwd(bits, G):
                     stop = True
                 else:
                     p = end
-                    nf = G
+                    nf = GR
                     batches += 1
         seeds.append((off, ln))
         i = off + ln + 3
@@ -153,16 +155,16 @@ def main():
         allbits.append(exist_bits(c, l, sbm, ek0, ek1, mask))
         allbits.append(exist_bits((3 - c)[::-1].copy(), l, sbm, ek0, ek1, mask))
     print(f"{nr} reads, {tot_pos} k-mer positions, exist rate {sum(b.sum() for b in allbits) / tot_pos:.3f}")
-    for G in (1, 4, 8, 16, 32):
+    for G, GR in ((4, 4), (8, 8), (16, 16), (32, 32), (8, 16), (12, 16), (16, 8), (6, 16), (16, 32), (8, 32)):
         P = B = N = 0
         maxb = 0
         for b in allbits:
-            p, bt, nd, _ = scan_fwd(b, G)
+            p, bt, nd, _ = scan_fwd(b, G, GR)
             P += p
             B += bt
             N += nd
             maxb = max(maxb, bt)
-        print(f"G={G:2d}: probes {P / tot_pos:.3f} of all positions, needed {N / tot_pos:.3f}, "
+        print(f"grid {G:2d} run {GR:2d}: probes {P / tot_pos:.3f} of all positions, needed {N / tot_pos:.3f}, "
               f"batches/strand {B / len(allbits):.0f} (max {maxb})")
 
 
