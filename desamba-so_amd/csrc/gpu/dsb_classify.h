@@ -350,7 +350,7 @@ DSB_HD uint32_t dsb_search_exist(const uint64_t *ex_, uint32_t l_kmer_v, dsb_see
  * back neighbours + the first G-2 positions of the run after it; RUN batches continue the run
  * G positions at a time.  Every batch's bits are probed together (one round trip), the state
  * update below is the reference loop's over those bits, so the seeds equal dsb_search_exist's
- * for any G >= 4 (tests/emu/isl_check.cpp replays both over the same bits). */
+ * for any batch sizes >= 4 (tests/emu/isl_check.cpp replays both over the same bits). */
 #ifndef DSB_ISLAND_G
 #define DSB_ISLAND_G 16 /* lanes per strand (k_island_g); 0: k_seed's exist bits + the two-lane k_island */
 #endif
@@ -368,36 +368,37 @@ DSB_HD void dsb_isl_init(dsb_isl_t *s, int nk, int fwd, int live)
 	s->mode = (live && (fwd ? s->i < nk : s->i >= 0)) ? DSB_ISL_GRID : DSB_ISL_DONE;
 }
 
-/* the position lane gl of the strand's G lanes probes in this batch; -1: none */
-template <int G>
+/* the position lane gl of the strand's lanes probes in this batch (GG positions per grid
+ * batch, GR per run batch); -1: none */
+template <int GG, int GR>
 DSB_HD int dsb_isl_pos(const dsb_isl_t *s, int gl)
 {
 	int d = s->fwd ? 1 : -1, q;
 	switch (s->mode) {
-	case DSB_ISL_GRID: q = s->i + 3 * d * gl; break;
-	case DSB_ISL_RUN1: q = gl < 2 ? s->h - d * (gl + 1) : s->h + d * (gl - 1); break;
-	case DSB_ISL_RUN: q = s->p + d * gl; break;
+	case DSB_ISL_GRID: if (gl >= GG) return -1; q = s->i + 3 * d * gl; break;
+	case DSB_ISL_RUN1: if (gl >= GR) return -1; q = gl < 2 ? s->h - d * (gl + 1) : s->h + d * (gl - 1); break;
+	case DSB_ISL_RUN: if (gl >= GR) return -1; q = s->p + d * gl; break;
 	default: return -1;
 	}
 	return (q >= 0 && q < s->nk) ? q : -1;
 }
 
 /* the lowest and highest position the batch probes (lo > hi: none) */
-template <int G>
+template <int GG, int GR>
 DSB_HD void dsb_isl_span(const dsb_isl_t *s, int *lo, int *hi)
 {
 	int a = 0, b = -1;
 	if (s->fwd) {
 		switch (s->mode) {
-		case DSB_ISL_GRID: a = s->i; b = s->i + 3 * DSB_MIN(G - 1, (s->nk - 1 - s->i) / 3); break;
-		case DSB_ISL_RUN1: a = s->h - 2; b = DSB_MIN(s->h + G - 2, s->nk - 1); break;
-		case DSB_ISL_RUN: a = s->p; b = DSB_MIN(s->p + G - 1, s->nk - 1); break;
+		case DSB_ISL_GRID: a = s->i; b = s->i + 3 * DSB_MIN(GG - 1, (s->nk - 1 - s->i) / 3); break;
+		case DSB_ISL_RUN1: a = s->h - 2; b = DSB_MIN(s->h + GR - 2, s->nk - 1); break;
+		case DSB_ISL_RUN: a = s->p; b = DSB_MIN(s->p + GR - 1, s->nk - 1); break;
 		}
 	} else {
 		switch (s->mode) {
-		case DSB_ISL_GRID: b = s->i; a = s->i - 3 * DSB_MIN(G - 1, s->i / 3); break;
-		case DSB_ISL_RUN1: b = s->h + 2; a = DSB_MAX(s->h - (G - 2), 0); break;
-		case DSB_ISL_RUN: b = s->p; a = DSB_MAX(s->p - (G - 1), 0); break;
+		case DSB_ISL_GRID: b = s->i; a = s->i - 3 * DSB_MIN(GG - 1, s->i / 3); break;
+		case DSB_ISL_RUN1: b = s->h + 2; a = DSB_MAX(s->h - (GR - 2), 0); break;
+		case DSB_ISL_RUN: b = s->p; a = DSB_MAX(s->p - (GR - 1), 0); break;
 		}
 	}
 	*lo = a;
@@ -406,7 +407,7 @@ DSB_HD void dsb_isl_span(const dsb_isl_t *s, int *lo, int *hi)
 
 /* one batch: bit g of mb = exist bit of dsb_isl_pos(s, g).  Returns 1 when a seed closes
  * (*so, *sl = CLY_seed offset / len as search_exist_kmer_M2 stores them). */
-template <int G>
+template <int GG, int GR>
 DSB_HD int dsb_isl_step(dsb_isl_t *s, uint32_t mb, uint32_t *so, uint32_t *sl)
 {
 	int d = s->fwd ? 1 : -1;
@@ -417,7 +418,7 @@ DSB_HD int dsb_isl_step(dsb_isl_t *s, uint32_t mb, uint32_t *so, uint32_t *sl)
 			s->ln = 1;
 			s->mode = DSB_ISL_RUN1;
 		} else {
-			s->i += 3 * d * G;
+			s->i += 3 * d * GG;
 			if (s->fwd ? s->i >= s->nk : s->i < 0)
 				s->mode = DSB_ISL_DONE;
 		}
@@ -438,7 +439,7 @@ DSB_HD int dsb_isl_step(dsb_isl_t *s, uint32_t mb, uint32_t *so, uint32_t *sl)
 		g = 2;
 		cur = s->h + d;
 	}
-	for (; g < G; g++, cur += d) { /* the run: i + j < l_kmer_v / j <= i, len > 60 ends it */
+	for (; g < GR; g++, cur += d) { /* the run: i + j < l_kmer_v / j <= i, len > 60 ends it */
 		if (s->fwd ? cur >= s->nk : cur < 0) { stop = 1; break; }
 		if (!((mb >> g) & 1)) { stop = 1; break; }
 		if (++s->ln > 60) { stop = 1; break; }
@@ -802,6 +803,85 @@ DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t
 	*len_ = len;
 }
 
+/* get_new_ed split into steps (dsb_ned_*), so that a caller can advance two independent
+ * extensions in one loop and have both chains' loads in flight together (dsb_map_item: the
+ * left and right extension of a REF_POS entry).  Same bytes, compares and result as
+ * dsb_get_new_ed. */
+typedef struct {
+	dsb_w32 T, Q;           /* get_new_ed's t_buff / q_buff: bytes past len keep earlier values */
+	uint64_t ql, qh, t_off;
+	const uint8_t *q;
+	int32_t q_off;
+	uint32_t len, max_len, ext;
+	int fwd, go;
+} dsb_ned_t;
+
+DSB_HD void dsb_ned_load(dsb_read_ws *w, dsb_ned_t *e, const uint8_t *q_b)
+{
+	if (e->fwd) {
+		uint64_t lo, hi;
+		dsb_rev16(q_b + e->q_off, &lo, &hi);
+		dsb_w32_put(e->Q, e->len, lo, hi);
+		e->ql = e->Q.b;
+		e->qh = e->Q.c;
+	} else {
+		e->ql = dsb_ld8u(e->q);
+		e->qh = dsb_ld8u(e->q + 8);
+	}
+	dsb_get_ref_r(w, e->T, e->t_off, e->len, !e->fwd);
+}
+
+DSB_HD void dsb_ned_start(dsb_read_ws *w, dsb_ned_t *e, const uint8_t *q_b, int32_t q_off, uint64_t t_off, uint32_t l_read,
+			  int is_FWD)
+{
+	e->fwd = is_FWD;
+	e->ext = 0;
+	e->T = dsb_w32_splat(DSB_STACK_PATTERN);
+	e->Q = e->T;
+	e->t_off = t_off;
+	if (is_FWD) {
+		if (q_off < 0)
+			q_off = 0;
+		e->max_len = (uint32_t)q_off;
+		e->q = q_b;
+	} else {
+		e->max_len = l_read - (uint32_t)q_off;
+		e->q = q_b + q_off;
+	}
+	e->q_off = q_off;
+	e->len = DSB_MIN(12u, e->max_len);
+	dsb_ned_load(w, e, q_b);
+	e->go = e->len > 0 && (e->T.b & 0xff) == (e->ql & 0xff);
+}
+
+/* one trip of get_new_ed's do-while: extend over the matching prefix and reload */
+DSB_HD void dsb_ned_step(dsb_read_ws *w, dsb_ned_t *e, const uint8_t *q_b)
+{
+	uint32_t mtc = dsb_w32_mismatch(e->T, e->ql, e->qh, e->len);
+	if (mtc == 0) {
+		e->go = 0;
+		return;
+	}
+	e->ext += mtc;
+	e->max_len -= mtc;
+	e->len = DSB_MIN(12u, e->max_len);
+	if (e->fwd) {
+		e->q_off -= (int32_t)mtc;
+		e->t_off -= mtc;
+	} else {
+		e->t_off += mtc;
+		e->q += mtc;
+	}
+	dsb_ned_load(w, e, q_b);
+}
+
+DSB_HD uint32_t dsb_ned_finish(const dsb_ned_t *e)
+{
+	/* !fwd: lv_extd terminates a copy of the read's bytes (q - 8 .. q + 24) */
+	dsb_w32 Q = e->fwd ? e->Q : dsb_w32_load(e->q - 8);
+	return (uint32_t)dsb_lv_extd_r(e->T, (int32_t)e->len, Q, (int32_t)e->len);
+}
+
 typedef struct { uint8_t *bin_read; uint32_t read_L; uint16_t seed_ID; uint32_t direction; } dsb_seedinfo_t;
 
 /* Q_MEM[l]: the reference reads past its 2000 entries for exact matches >= 2000 bp
@@ -972,23 +1052,54 @@ DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, c
 	uint16_t am_mtch = cx->am_mtch;
 	int16_t am_score = cx->am_score;
 	uint8_t am_ll = cx->am_ll, am_le = cx->am_le, am_rl = cx->am_rl, am_re = cx->am_re;
-	uint32_t ed_l, ed_r, len_l, len_r;
-	uint32_t l_m_ext_l = 0, l_m_ext_r;
+	uint32_t l_m_ext_l = 0;
+	uint32_t ref_id = DSB_RP_REF(rp);
+	uint64_t seq_off = dsb_gld(ix->ref_seq_offset + ref_id); /* issued with the extensions' loads */
 	if (cx->ref_l || cx->ref_r) {
-		if (cx->ref_l) {
-			dsb_get_new_ed(w, s_i->bin_read, &ed_l, &len_l, &l_m_ext_l, cx->q_off, DSB_RP_OFF(rp) + cx->u_off - 1,
-				       s_i->read_L, 1);
-			am_ll = (uint8_t)len_l;
-			am_le = (uint8_t)ed_l;
-		}
-		am_mtch = (uint16_t)(cx->l_m + l_m_ext_l);
-		if (cx->ref_r) {
-			l_m_ext_r = 0;
-			dsb_get_new_ed(w, s_i->bin_read, &ed_r, &len_r, &l_m_ext_r, cx->q_off + cx->l_m + 1,
-				       DSB_RP_OFF(rp) + cx->u_off + cx->l_m, s_i->read_L, 0);
-			am_rl = (uint8_t)len_r;
-			am_re = (uint8_t)ed_r;
-			am_mtch = (uint16_t)(am_mtch + l_m_ext_r);
+#ifndef DSB_NED_PAIR
+#define DSB_NED_PAIR 0 /* measured: fast seeding 44.9 -> 45.8 ms with the pair (registers at the 256 cap): off */
+#endif
+		if (DSB_NED_PAIR) {
+			/* the left and right extensions are independent: both chains advance in one loop */
+			dsb_ned_t L, R;
+			L.go = R.go = 0;
+			if (cx->ref_l)
+				dsb_ned_start(w, &L, s_i->bin_read, cx->q_off, DSB_RP_OFF(rp) + cx->u_off - 1, s_i->read_L, 1);
+			if (cx->ref_r)
+				dsb_ned_start(w, &R, s_i->bin_read, cx->q_off + cx->l_m + 1, DSB_RP_OFF(rp) + cx->u_off + cx->l_m,
+					      s_i->read_L, 0);
+			while (L.go || R.go) {
+				if (L.go) dsb_ned_step(w, &L, s_i->bin_read);
+				if (R.go) dsb_ned_step(w, &R, s_i->bin_read);
+			}
+			if (cx->ref_l) {
+				am_le = (uint8_t)dsb_ned_finish(&L);
+				am_ll = (uint8_t)L.len;
+				l_m_ext_l = L.ext;
+			}
+			am_mtch = (uint16_t)(cx->l_m + l_m_ext_l);
+			if (cx->ref_r) {
+				am_re = (uint8_t)dsb_ned_finish(&R);
+				am_rl = (uint8_t)R.len;
+				am_mtch = (uint16_t)(am_mtch + R.ext);
+			}
+		} else {
+			uint32_t ed_l, ed_r, len_l, len_r, l_m_ext_r;
+			if (cx->ref_l) {
+				dsb_get_new_ed(w, s_i->bin_read, &ed_l, &len_l, &l_m_ext_l, cx->q_off, DSB_RP_OFF(rp) + cx->u_off - 1,
+					       s_i->read_L, 1);
+				am_ll = (uint8_t)len_l;
+				am_le = (uint8_t)ed_l;
+			}
+			am_mtch = (uint16_t)(cx->l_m + l_m_ext_l);
+			if (cx->ref_r) {
+				l_m_ext_r = 0;
+				dsb_get_new_ed(w, s_i->bin_read, &ed_r, &len_r, &l_m_ext_r, cx->q_off + cx->l_m + 1,
+					       DSB_RP_OFF(rp) + cx->u_off + cx->l_m, s_i->read_L, 0);
+				am_rl = (uint8_t)len_r;
+				am_re = (uint8_t)ed_r;
+				am_mtch = (uint16_t)(am_mtch + l_m_ext_r);
+			}
 		}
 		am_score = (int16_t)(dsb_qmem(ix, am_mtch) + dsb_gld(Q_LV + (am_le * DSB_LV_DIM + am_ll)) + dsb_gld(Q_LV + (am_re * DSB_LV_DIM + am_rl)));
 		if (am_score < DSB_MIN_S_2)
@@ -997,8 +1108,8 @@ DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, c
 	a->direction = (uint8_t)s_i->direction;
 	a->index_in_read = cx->q_off + 1 - l_m_ext_l;
 	a->global_offset = DSB_RP_OFF(rp) + cx->u_off - l_m_ext_l;
-	a->ref_ID = DSB_RP_REF(rp);
-	a->ref_offset = (uint32_t)(a->global_offset - dsb_gld(ix->ref_seq_offset + a->ref_ID));
+	a->ref_ID = ref_id;
+	a->ref_offset = (uint32_t)(a->global_offset - seq_off);
 	a->mtch_len = am_mtch;
 	a->score = am_score;
 	a->left_len = am_ll; a->left_ED = am_le; a->rigt_len = am_rl; a->rigt_ED = am_re;
