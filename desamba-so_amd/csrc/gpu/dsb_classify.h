@@ -1248,6 +1248,12 @@ DSB_HDN void dsb_fast_classify(dsb_read_ws *w, const dsb_sdir_t *s_d)
 #ifndef DSB_SEED_PRE
 #define DSB_SEED_PRE 1
 #endif
+#ifndef DSB_SM_LPT
+#define DSB_SM_LPT 1 /* pass 0 hands seeds out longest first */
+#endif
+#ifndef DSB_SM_LPT_CH
+#define DSB_SM_LPT_CH 2 /* top-seed lengths held in registers for the hand-out sort (x 64 seeds) */
+#endif
 #ifndef DSB_SM_MAP_BATCH
 #define DSB_SM_MAP_BATCH 64
 #endif
@@ -1344,9 +1350,10 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	int n_top = 0, total = 0;
 	uint8_t *bin_read = w->bin + (s_d->strand ? w->L : 0);
 	/* ---- top seeds, in order (tix) */
-	/* the read-hash region is free while seeding (>= 16 L bytes; n_sv <= L/3 + 1): 2 record words,
-	 * the pass-1 list and the top-seed list per seed */
+	/* the read-hash region is free while seeding (>= 16 L bytes; n_sv <= L/3 + 1): 5 words per seed
+	 * — 2 record words, the pass-1 list, the top-seed list and the pass-0 hand-out order */
 	uint32_t *rec = w->hh[0], *klist = rec + 2 * (uint64_t)n_sv, *tix = rec + 3 * (uint64_t)n_sv;
+	uint32_t *hand = rec + 4 * (uint64_t)n_sv; /* pass-0 hand-out order (DSB_SM_LPT) */
 	uint32_t m = 0;
 	for (uint32_t gb = 0; gb < n_sv; gb += DSB_WV) {
 		uint32_t ci = gb + lane;
@@ -1362,6 +1369,41 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 		if (SLOW)
 			w->fast_classify = 0;
 		return;
+	}
+	/* Pass 0 hands the top seeds out longest first (a seed's FM / map work grows with its
+	 * length), so that the long ones do not start in the last lanes to free up; ties in seed
+	 * order.  The output does not depend on the hand-out order: every seed's anchors and skip
+	 * trigger are recorded per seed and compacted in seed order below. */
+	if (DSB_SM_LPT) {
+		auto seed_len = [&](uint32_t q) -> uint32_t {
+			return q < m ? DSB_MIN(w->seeds[s_d->seed_off + tix[q]].len, 63u) : 64u;
+		};
+		uint32_t slen[DSB_SM_LPT_CH];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+		for (int c = 0; c < DSB_SM_LPT_CH; c++)
+			slen[c] = seed_len((uint32_t)c * DSB_WV + lane);
+		uint32_t pos = 0;
+		auto place = [&](uint32_t q, int t) {
+			uint64_t bm = dsb_wballot(t);
+			if (t) {
+				uint64_t below = lane == 0 ? 0 : (bm & (~0ull >> (64 - lane)));
+				hand[pos + (uint32_t)__builtin_popcountll(below)] = q;
+			}
+			pos += (uint32_t)__builtin_popcountll(bm);
+		};
+		for (uint32_t b = 64; b-- > 0;) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+			for (int c = 0; c < DSB_SM_LPT_CH; c++)
+				if ((uint32_t)c * DSB_WV < m)
+					place((uint32_t)c * DSB_WV + lane, slen[c] == b);
+			for (uint32_t gb = DSB_SM_LPT_CH * DSB_WV; gb < m; gb += DSB_WV)
+				place(gb + lane, seed_len(gb + lane) == b);
+		}
+		dsb_wsync();
 	}
 	dsb_anchor_t *anc0 = w->anc;
 	uint32_t n0 = w->n_anc, cap0 = w->cap.anc, of0 = w->overflow;
@@ -1404,7 +1446,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	}
 #define DSB_SM_START_SEED(K)                                                   \
 	do {                                                                   \
-		k = pr ? klist[K] : (K);                                       \
+		k = pr ? klist[K] : (DSB_SM_LPT ? hand[K] : (K));              \
 		ci = tix[k];                                                   \
 		const dsb_seed_t *c_sv_ = w->seeds + s_d->seed_off + ci;       \
 		seed_off = c_sv_->offset;                                      \
