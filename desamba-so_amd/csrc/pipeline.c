@@ -5,7 +5,7 @@
  * src/lib/kthread.c:114-197): read <= 5000 reads / 10 Mbp, classify them with kt_for over
  * thread_num pthreads, write the records in input order.  Here the steps are:
  *
- *   parse    (calling thread)  kt_pipeline batches of the resident text, as record views
+ *   parse    (one thread)      kt_pipeline batches of the resident text, as record views
  *                              (fastq.c), grouped into GPU batches of up to DSB_PIPE_READS
  *                              reads / DSB_PIPE_MBP Mbp
  *   stage    (one thread/GPU)  bases gathered into pinned staging by the host pool, copied on
@@ -13,7 +13,7 @@
  *   classify (one thread/GPU)  the kernels (kernels.hip batch_run); the carried max_read_l
  *                              (cly.c:2953) passes from batch to batch, across GPUs, between
  *                              part A and part B of each batch
- *   format   (one thread)      SAM / SAM_FULL / DES / DES_FULL records of each batch in input
+ *   format   (calling thread)  SAM / SAM_FULL / DES / DES_FULL records of each batch in input
  *                              order, formatted in parallel by the host pool into one growing
  *                              output buffer
  *
@@ -64,6 +64,9 @@ typedef struct {
 	dsb_gpu_timing gt;
 	double ms_parse, ms_gather, ms_format, ms_wait_gpu;
 	uint64_t n_batches;
+	/* parser thread */
+	dsb_parser *ps;
+	uint64_t max_reads, max_bases, depth;
 } pipe_t;
 
 typedef struct {
@@ -327,6 +330,68 @@ static int format_batch(pipe_t *p, pbatch *b)
 	return 0;
 }
 
+/* ---------------------------------------------------------------- parse */
+/* parser thread: GPU batches of the text in input order while fewer than `depth` batches are
+ * alive, so that parsing batch k+1 overlaps formatting batch k on the calling thread */
+static void *parser_main(void *arg)
+{
+	pipe_t *p = arg;
+	uint64_t seq = 0;
+	for (;;) {
+		pthread_mutex_lock(&p->mu);
+		while (!p->failed && p->n_parsed - p->n_formatted >= p->depth)
+			pthread_cond_wait(&p->cv, &p->mu);
+		if (p->failed)
+			break; /* mu held */
+		pthread_mutex_unlock(&p->mu);
+		double tp = now_ms();
+		pbatch *b = calloc(1, sizeof(pbatch));
+		/* the first batch is a quarter size, so the GPU starts sooner */
+		uint64_t mr = seq == 0 ? (p->max_reads + 3) / 4 : p->max_reads;
+		uint64_t got = b ? dsb_parser_next(p->ps, &b->reads, mr, p->max_bases) : 0;
+		double dt = now_ms() - tp;
+		pthread_mutex_lock(&p->mu);
+		p->ms_parse += dt;
+		if (!got) {
+			if (b) {
+				free(b->reads.rec);
+				free(b);
+			}
+			break; /* parse_done below */
+		}
+		b->seq = seq++;
+		if (b->seq >= p->by_seq_cap) {
+			uint64_t c = p->by_seq_cap ? p->by_seq_cap * 2 : 64;
+			pbatch **q = realloc(p->by_seq, c * sizeof(pbatch *));
+			if (!q) {
+				pthread_mutex_unlock(&p->mu);
+				free(b->reads.rec);
+				free(b);
+				fail(p, "out of memory parsing the input");
+				pthread_mutex_lock(&p->mu);
+				break;
+			}
+			p->by_seq = q;
+			memset(p->by_seq + p->by_seq_cap, 0, (c - p->by_seq_cap) * sizeof(pbatch *));
+			p->by_seq_cap = c;
+		}
+		p->by_seq[b->seq] = b;
+		if (p->parsed_tail)
+			p->parsed_tail->next = b;
+		else
+			p->parsed_head = b;
+		p->parsed_tail = b;
+		p->n_parsed++;
+		pthread_cond_broadcast(&p->cv);
+		pthread_mutex_unlock(&p->mu);
+	}
+	/* mu held */
+	p->parse_done = 1;
+	pthread_cond_broadcast(&p->cv);
+	pthread_mutex_unlock(&p->mu);
+	return NULL;
+}
+
 /* ---------------------------------------------------------------- driver */
 int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint64_t text_n, int format, int max_sec_N,
 			  int *max_read_l, int stats_on, char **output, uint64_t *output_n, dsb_pipe_timing *pt,
@@ -350,11 +415,11 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 	p->carry0 = *max_read_l;
 	pthread_mutex_init(&p->mu, NULL);
 	pthread_cond_init(&p->cv, NULL);
-	uint64_t max_reads = env_u64("DSB_PIPE_READS", 25000);
-	uint64_t max_bases = env_u64("DSB_PIPE_MBP", 400) * 1000000ull;
-	uint64_t depth = env_u64("DSB_PIPE_DEPTH", 2 + 2 * (uint64_t)n_dev);
-	if (max_reads == 0) max_reads = 1;
-	if (depth < 2) depth = 2;
+	p->max_reads = env_u64("DSB_PIPE_READS", 25000);
+	p->max_bases = env_u64("DSB_PIPE_MBP", 400) * 1000000ull;
+	p->depth = env_u64("DSB_PIPE_DEPTH", 2 + 2 * (uint64_t)n_dev);
+	if (p->max_reads == 0) p->max_reads = 1;
+	if (p->depth < 2) p->depth = 2;
 	/* SAM_FULL output is about the input's size */
 	p->out_m = text_n + text_n / 8 + (1u << 20);
 	p->out = malloc(p->out_m);
@@ -363,7 +428,8 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 		return -1;
 	}
 	out_hugepages(p->out, p->out_m);
-	pthread_t th[2 * DSB_MAX_GPUS];
+	p->ps = dsb_parser_new(text, text_n);
+	pthread_t th[2 * DSB_MAX_GPUS], pth;
 	dev_arg args[DSB_MAX_GPUS];
 	for (int d = 0; d < n_dev; d++) {
 		args[d].p = p;
@@ -371,69 +437,25 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 		pthread_create(th + 2 * d, NULL, stager, args + d);
 		pthread_create(th + 2 * d + 1, NULL, runner, args + d);
 	}
-	dsb_parser *ps = dsb_parser_new(text, text_n);
-	uint64_t seq = 0;
-	int parse_open = 1;
+	pthread_create(&pth, NULL, parser_main, p);
+	/* format each batch in input order once it is classified */
 	for (;;) {
-		/* parse while fewer than `depth` batches are alive */
-		pthread_mutex_lock(&p->mu);
-		while (parse_open && !p->failed && p->n_parsed - p->n_formatted < depth) {
-			pthread_mutex_unlock(&p->mu);
-			double tp = now_ms();
-			pbatch *b = calloc(1, sizeof(pbatch));
-			/* the first batch is a quarter size, so the GPU starts sooner */
-			uint64_t mr = seq == 0 ? (max_reads + 3) / 4 : max_reads;
-			uint64_t got = dsb_parser_next(ps, &b->reads, mr, max_bases);
-			double dt = now_ms() - tp;
-			pthread_mutex_lock(&p->mu);
-			p->ms_parse += dt;
-			if (!got) {
-				free(b->reads.rec);
-				free(b);
-				parse_open = 0;
-				p->parse_done = 1;
-				pthread_cond_broadcast(&p->cv);
-				break;
-			}
-			b->seq = seq++;
-			if (b->seq >= p->by_seq_cap) {
-				uint64_t c = p->by_seq_cap ? p->by_seq_cap * 2 : 64;
-				p->by_seq = realloc(p->by_seq, c * sizeof(pbatch *));
-				memset(p->by_seq + p->by_seq_cap, 0, (c - p->by_seq_cap) * sizeof(pbatch *));
-				p->by_seq_cap = c;
-			}
-			p->by_seq[b->seq] = b;
-			if (p->parsed_tail)
-				p->parsed_tail->next = b;
-			else
-				p->parsed_head = b;
-			p->parsed_tail = b;
-			p->n_parsed++;
-			pthread_cond_broadcast(&p->cv);
-		}
-		/* format the next batch in input order once it is classified */
-		if (p->n_formatted == p->n_parsed && !parse_open) {
-			pthread_mutex_unlock(&p->mu);
-			break;
-		}
 		double tw = now_ms();
 		pbatch *b = NULL;
+		pthread_mutex_lock(&p->mu);
 		while (!p->failed) {
 			b = p->n_formatted < p->n_parsed ? p->by_seq[p->n_formatted] : NULL;
 			if (b && b->classified)
 				break;
 			b = NULL;
-			if (parse_open && p->n_parsed - p->n_formatted < depth)
-				break; /* room to parse more first */
+			if (p->parse_done && p->n_formatted == p->n_parsed)
+				break;
 			pthread_cond_wait(&p->cv, &p->mu);
 		}
 		p->ms_wait_gpu += now_ms() - tw;
-		int failed = p->failed;
 		pthread_mutex_unlock(&p->mu);
-		if (failed)
-			break;
 		if (!b)
-			continue;
+			break; /* failed, or everything formatted */
 		double tf = now_ms();
 		if (format_batch(p, b)) {
 			fail(p, "out of memory formatting the output");
@@ -450,6 +472,8 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 		pthread_mutex_unlock(&p->mu);
 		free(b);
 	}
+	pthread_join(pth, NULL);
+	uint64_t seq = p->n_parsed;
 	pthread_mutex_lock(&p->mu);
 	p->parse_done = 1;
 	pthread_cond_broadcast(&p->cv);
@@ -492,11 +516,11 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 		pt->n_batches = p->n_batches;
 		pt->n_devices = (uint64_t)n_dev;
 		uint64_t nf = 0, ns = 0;
-		dsb_parser_stats(ps, &nf, &ns);
+		dsb_parser_stats(p->ps, &nf, &ns);
 		pt->n_view_records = nf;
 		pt->n_copied_records = ns;
 	}
-	dsb_parser_free(ps);
+	dsb_parser_free(p->ps);
 	for (uint64_t t = 0; t < p->n_tbuf; t++)
 		free(p->tbuf[t].s);
 	free(p->tbuf);
