@@ -107,7 +107,6 @@ typedef struct {
 	uint64_t *lds_key;      /* wave chaining: anchor sort keys / ids in LDS (DSB_SORT_LDS entries), or 0 */
 	uint32_t *lds_id;
 	uint16_t *lds_cand;     /* wave scoring: 64 candidate slots of the register k-mer match (DSB_MATCH_BF), or 0 */
-	uint8_t *lds_q;         /* wave scoring: DSB_QCOPY_BYTES of LDS for a window's read range (DSB_QCOPY), or 0 */
 	uint8_t *lds_hb;        /* wave read-hash build: DSB_HB_LDS lane-id bytes in LDS (key groups of a chunk), or 0 */
 	uint32_t *hh[2], *hn[2]; /* read 9-mer hash per strand: list heads per key, one node per position */
 	dsb_sch_t *sch;         /* 256 + 2*400 */
@@ -2876,40 +2875,6 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			}
 			return kmer;
 		};
-#ifndef DSB_QCOPY
-#define DSB_QCOPY 0
-#endif
-#ifndef DSB_BIN_TAIL
-#define DSB_BIN_TAIL 256 /* bytes after R in the read buffer (dsb_ws.h) */
-#endif
-#ifndef DSB_QCOPY_BYTES
-#define DSB_QCOPY_BYTES 768
-#endif
-		/* The candidates' extensions (MEM_search over the read bytes) read the window's read
-		 * range [q_bg, q_ed] and a little around it: when that range fits, the wave copies it
-		 * once into LDS (one coalesced load per lane, issued with the probes' head loads), and
-		 * an extension whose bytes lie inside the copy reads LDS instead of making its own
-		 * dependent global round trips; the others read the read buffer as before.  Same bytes
-		 * either way. */
-		const uint8_t *qv = q_str; /* q_str or its LDS copy: qv + x is read byte x */
-		int64_t qv_lo = 1, qv_hi = 0; /* read bytes the copy holds */
-#if DSB_QCOPY
-		/* the copy must stay inside the read buffer (F | R + the tail guard) */
-		const uint8_t *qca = (const uint8_t *)((uintptr_t)(q_str + q_bg - 32) & ~(uintptr_t)7);
-		if (w->lds_q && q_bg <= q_ed && (int64_t)q_ed - (int64_t)q_bg + 128 <= DSB_QCOPY_BYTES - 16 &&
-		    (int64_t)q_bg >= 32 && qca + DSB_QCOPY_BYTES <= w->bin + 2ull * w->L + DSB_BIN_TAIL) {
-			const uint64_t *src = (const uint64_t *)qca;
-			uint64_t *dst = (uint64_t *)w->lds_q;
-			for (uint32_t k = lane; k < DSB_QCOPY_BYTES / 8; k += DSB_WV)
-				dst[k] = src[k];
-			dsb_wsync();
-			qv = w->lds_q - (qca - q_str);
-			qv_lo = (int64_t)(qca - q_str);
-			qv_hi = qv_lo + DSB_QCOPY_BYTES - 1;
-		}
-#endif
-		/* read base for bytes [a, b] of the read: the copy when it holds them */
-		auto qsel = [&](int64_t a, int64_t b) -> const uint8_t * { return (a >= qv_lo && b <= qv_hi) ? qv : q_str; };
 #ifndef DSB_MATCH_BF
 #define DSB_MATCH_BF 0 /* measured: 3 -> scoring 56.7 -> 60.6 ms, 2 -> 59.2 ms (the compare loop and its spills cost more than the head loads): off */
 #endif
@@ -3072,13 +3037,12 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 					dsb_spd_t e;
 					int ok = 0;
 					if (isForward) {
-						int64_t xb = (int64_t)q_pos - 1, xf = (int64_t)q_pos + DSB_S_A_KMER_L;
-						int back_len = dsb_MEM_search(qsel(xb - 28, xb + 16) + xb, c_t_str - 1, 0, 4);
+						int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, 4);
 						if (back_len < 4 || i == 4) {
 							uint32_t max_search = q_ed - q_pos - 1;
 							max_search = DSB_MIN(max_search, t_len - i - 1) + DSB_OVER_SEARCH;
-							int forward_len = dsb_MEM_search(qsel(xf - 8, xf + (int64_t)max_search + 16) + xf,
-											 c_t_str + DSB_S_A_KMER_L, 1, (int)max_search);
+							int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L,
+											 1, (int)max_search);
 							int total_len = back_len + forward_len + 1;
 							if (total_len >= 4) {
 								e.len = total_len;
@@ -3088,13 +3052,11 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 							}
 						}
 					} else {
-						int64_t xb = (int64_t)q_pos - 1, xf = (int64_t)q_pos + DSB_S_A_KMER_L;
-						int forward_len = dsb_MEM_search(qsel(xf - 8, xf + 20) + xf, c_t_str + DSB_S_A_KMER_L, 1, 4);
+						int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L, 1, 4);
 						if (forward_len < 4 || i == 4) {
 							uint32_t max_search = q_pos;
 							max_search = DSB_MIN(max_search, (uint32_t)(c_t_str - t_str)) + DSB_OVER_SEARCH;
-							int back_len = dsb_MEM_search(qsel(xb - (int64_t)max_search - 24, xb + 16) + xb, c_t_str - 1, 0,
-										      (int)max_search);
+							int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, (int)max_search);
 							int total_len = back_len + forward_len + 1;
 							if (total_len >= 4) {
 								e.len = total_len;

@@ -414,11 +414,6 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 			static_assert(DSB_WIN_LDS_BYTES <= DSB_DELA_CAND_OFF && DSB_DELA_CAND_OFF + 128 <= DSB_DELA_LDS_BYTES,
 				      "candidate slots must not overlap the windows");
 			w.lds_cand = (uint16_t *)((uint8_t *)dela_lds + DSB_DELA_CAND_OFF);
-			/* a window's read range (DSB_QCOPY): the LDS past the windows */
-			static_assert(DSB_WIN_LDS_BYTES + DSB_QCOPY_BYTES <= DSB_DELA_LDS_BYTES && (DSB_WIN_LDS_BYTES & 7) == 0,
-				      "the read-range copy must fit past the windows");
-			static_assert(!(DSB_MATCH_BF && DSB_QCOPY), "the candidate slots share the read-range copy's LDS");
-			w.lds_q = (uint8_t *)dela_lds + DSB_WIN_LDS_BYTES;
 			dsb_phase<true>(&w, &f, ph);
 		} else
 			dsb_phase<true>(&w, &f, ph);
