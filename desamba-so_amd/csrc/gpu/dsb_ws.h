@@ -18,14 +18,7 @@
 
 DSB_HD uint64_t dsb_al(uint64_t x) { return (x + 255) & ~255ull; }
 
-DSB_HD int dsb_key_len(uint32_t q_len) /* build_hash_table_M2, src/cly.c:2179-2182 */
-{
-	int key_len = 10;
-	for (; key_len < 18; key_len++)
-		if ((int64_t)(1u << key_len) >= (int64_t)q_len)
-			break;
-	return key_len;
-}
+DSB_HD int dsb_key_len(uint32_t q_len) { return dsb_hash_kl(q_len); } /* the read hash's key bits */
 
 DSB_HD dsb_caps_t dsb_default_caps(uint32_t L, uint32_t scale)
 {
