@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Throughput of the MI355X classify path (BASELINE.json metric, config C1).
+"""Throughput of the MI355X classify path (BASELINE.json metric, config C2 at N = 1, C3 beyond).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--workload c1|c2|fixture]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--workload c2|c1|fixture]
                   [--mix ont|c4] [--index DIR]
 
 --gpus N without a torch.distributed launcher starts N rank processes itself (one per GPU,
@@ -14,10 +14,13 @@ results back on the host), then assign one taxon per read exactly as meta_analys
 (all_reduce over torch.distributed "nccl" when N > 1).  Reads shard across ranks (weak
 scaling: every rank classifies its own R reads); the index is replicated in each GPU's HBM.
 
-Workload C1: the >=50 Mbp synthetic family-structured proxy index (data/c1_index.txz,
-made by tools/make_c1_index.sh with the reference's own index builder; the demo human
-index is not available offline) + R = 100k reads per rank.  If data/c1_index.txz is
-absent the committed fixture index is used and config.workload says so.
+Workload C2 (the default; BASELINE configs[2], and per rank configs[3]): the C2 proxy index
+(tools/simulate.py preset c2: 495 Mbp, 286 M distinct 31-mers, so l_ek 17 / MASK_31 / 256 MB
+e-kmer tables; RefSeq itself is not available offline), built in this run by tools/proxy_build.py
+(simulate.py + this repository's desamba_index, ~60 s, cached under $TMPDIR) unless
+data/c2_index.txz is present, + R = 1M reads per rank, simulated by forked workers before the
+process touches a GPU.  Workload C1 (--workload c1): the 55.8 Mbp proxy of BASELINE configs[1]
+(data/c1_index.txz, made by the reference's own builder), usually with --reads 100000.
 
 The JSON line carries:
   roofline     the dominant kernel (the phase of classify part A with the largest HIP-event
@@ -28,13 +31,16 @@ The JSON line carries:
                workload (profiles/), or null.
   cpu_baseline the reference classifier (oracle/_ref/deSAMBA, built from the reference
                sources by oracle/Makefile) on the host cores, on a bounded sample of the
-               same reads, at -t nproc (the value) and -t 1, plus the reference's own
-               read_classify(thread_num = nproc) through dlopen (oracle/_ref/abi_time); the
-               GPU's primary taxids for the sample are compared with the reference's records
-               (taxid_mismatch); rank 0 at N = 1 only.
+               same reads, at -t <usable CPUs> (the cgroup quota) and at -t nproc, the faster
+               being the value, and at -t 1, plus the reference's own read_classify through
+               dlopen (oracle/_ref/abi_time); the GPU's primary taxids for the sample are
+               compared with the reference's records (taxid_mismatch), and the GPU's records of
+               the first reads with the hermetic reference's (oracle/_ref/herm_classify,
+               t3_mismatch); rank 0 at N = 1 only.
   dropin       the drop-in path end to end: one read_classify(idx, fastq, n, ...) call over
-               the whole batch (text in host memory -> SAM_FULL text in host memory: parse,
-               H2D, kernels, D2H, formatting), index preloaded; rank 0 at N = 1 only.
+               the first --dropin-reads reads of the batch (text in host memory -> SAM_FULL
+               text in host memory: parse, H2D, kernels, D2H, formatting), index preloaded,
+               checked against the batch path's records; rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -79,7 +85,7 @@ def _tmp():
     return os.environ.get("TMPDIR", "/tmp")
 
 
-# synthetic proxy indexes made by tools/make_proxy_index.sh with the reference's own builder
+# synthetic proxy indexes: shipped packed (data/, tests/golden/) or, for C2, built in the run
 WORKLOADS = {
     "c1": ("C1-proxy-56Mbp", os.path.join(ROOT, "data", "c1_index.txz")),
     "c2": ("C2-proxy-495Mbp-lek17", os.path.join(ROOT, "data", "c2_index.txz")),
@@ -87,12 +93,16 @@ WORKLOADS = {
 }
 
 
-def unpack_index(rank: int, workload: str = "c1") -> tuple[str, str]:
-    """-> (index dir, workload name).  Rank 0 unpacks, the others wait for it."""
+def unpack_index(rank: int, workload: str = "c2") -> tuple[str, str]:
+    """-> (index dir, workload name).  Rank 0 unpacks (or builds the C2 proxy), the others wait."""
     name, src = WORKLOADS[workload]
+    if workload == "c2" and not os.path.exists(src):
+        import proxy_build
+        d = proxy_build.ensure_proxy("c2", build=(rank == 0))
+        return d, name
     if not os.path.exists(src):
         if workload != "c1":
-            raise SystemExit(f"{src} missing: build it with tools/make_proxy_index.sh {workload}")
+            raise SystemExit(f"{src} missing")
         name, src = WORKLOADS["fixture"]
     st = os.stat(src)
     key = hashlib.sha1(f"{src}:{st.st_size}:{int(st.st_mtime)}".encode()).hexdigest()[:12]
@@ -119,22 +129,55 @@ def unpack_index(rank: int, workload: str = "c1") -> tuple[str, str]:
     return d, name
 
 
-def make_reads(index_dir: str, n: int, seed: int, mean_len: int, mix: str = "ont") -> bytes:
+def make_reads(index_dir: str, n: int, seed: int, mean_len: int, mix: str = "ont", world: int = 1) -> bytes:
     """Synthetic reads sampled from the index's own reference (tools/simulate.py): ONT-like
-    (lognormal mean `mean_len`), or BASELINE C4's mix (150 bp + 20 kb ONT, 1:1, interleaved)."""
-    path = os.path.join(_tmp(), f"dsb_reads_{os.path.basename(index_dir)}_{n}_{seed}_{mean_len}_{mix}.fq")
-    if not os.path.exists(path):
-        import simulate
-        t = time.time()
-        genomes = simulate.read_fasta_genomes_from_index(index_dir)
-        part = path + f".part{os.getpid()}"
-        gen = (simulate.simulate_c4_mix(genomes, n, seed) if mix == "c4"
-               else simulate.simulate_reads(genomes, n, seed, "ont", mean_len))
-        simulate.write_fastq(gen, part)
-        os.rename(part, path)
-        log(f"simulated {n} reads (seed {seed}) in {time.time() - t:.1f}s")
-    with open(path, "rb") as f:
-        return f.read()
+    (lognormal mean `mean_len`), or BASELINE C4's mix (150 bp + 20 kb ONT, 1:1, interleaved),
+    made in 10k-read chunks by forked workers (simulate_fastq_parallel; the text does not depend
+    on the worker count).  Cached under $TMPDIR when the disk has room.  Must run before this
+    process touches a GPU."""
+    path = os.path.join(_tmp(), f"dsb_reads_{os.path.basename(index_dir)}_{n}_{seed}_{mean_len}_{mix}_c10k.fq")
+    if os.path.exists(path):
+        with open(path, "rb") as f:
+            return f.read()
+    import proxy_build
+    import simulate
+    t = time.time()
+    genomes = simulate.read_fasta_genomes_from_index(index_dir)
+    workers = max(1, min(32, proxy_build.usable_cpus() // max(1, world)))
+    fq = simulate.simulate_fastq_parallel(genomes, n, seed, mix, mean_len, workers=workers)
+    del genomes
+    log(f"simulated {n} reads (seed {seed}, {len(fq) / 1e9:.2f} GB of FASTQ) on {workers} workers in {time.time() - t:.1f}s")
+    try:
+        import shutil
+        if shutil.disk_usage(_tmp()).free > 3 * len(fq) + (8 << 30):
+            part = path + f".part{os.getpid()}"
+            with open(part, "wb") as f:
+                f.write(fq)
+            os.rename(part, path)
+    except OSError:
+        pass
+    return fq
+
+
+def index_info(index_dir: str) -> dict:
+    """Size and e-kmer parameters of the index (set_ekmer_par, reference src/idx.c:966-982), plus how
+    it was made (tools/proxy_build.py's build.json when built in this run)."""
+    info = {}
+    try:
+        info["bytes"] = sum(os.path.getsize(os.path.join(index_dir, f)) for f in os.listdir(index_dir)
+                            if f.startswith("deSAMBA."))
+        with open(os.path.join(index_dir, "deSAMBA.exki"), "rb") as f:
+            ek = int.from_bytes(f.read(8), "little")
+        info["e_kmer_table_bytes"] = ek
+        info["l_ek"] = {1 << 27: 16, 1 << 28: 17, 1 << 29: 17, 1 << 30: 18, 1 << 31: 18, 1 << 32: 19,
+                        1 << 33: 19}.get(ek, 20)
+        bj = os.path.join(index_dir, "build.json")
+        if os.path.exists(bj):
+            with open(bj) as f:
+                info["built_in_run"] = json.load(f)
+    except OSError:
+        pass
+    return info
 
 
 def fastq_head(fq: bytes, n: int) -> bytes:
@@ -206,46 +249,85 @@ def n_bases(fq: bytes) -> int:
     return sum(len(l) for i, l in enumerate(fq.split(b"\n")) if i % 4 == 1)
 
 
+def t3_check(index_dir: str, sample: bytes, gpu_sam: bytes) -> dict | None:
+    """The hermetic reference (oracle/_ref/herm_classify: the reference's objects, fresh buffer
+    pools per read) on `sample`, every SAM record compared byte for byte with the
+    GPU's records of the same reads from the timed batch (T3)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "herm_classify")
+    if not os.path.exists(exe):
+        return None
+    with tempfile.TemporaryDirectory(dir=_tmp()) as d:
+        p = os.path.join(d, "t3.fq")
+        with open(p, "wb") as f:
+            f.write(sample)
+        t = time.time()
+        r = subprocess.run([exe, "--sam", index_dir, p], capture_output=True, timeout=900)
+    if r.returncode != 0:
+        log("herm_classify failed:", r.returncode, r.stderr[-400:])
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from samutil import compare
+    c = compare(r.stdout, gpu_sam)
+    return {"reads": c["reads"], "t3_mismatch": c["full_mismatch"], "taxid_mismatch": c["taxid_mismatch"],
+            "mapped_mismatch": c["mapped_mismatch"], "secs": round(time.time() - t, 1),
+            "oracle": "oracle/_ref/herm_classify --sam (hermetic reference build), first reads of the timed batch"}
+
+
 def cpu_baseline(index_dir: str, fq: bytes, n_sample: int, n_sample_t1: int, gpu_sam_sample: bytes | None):
     """The reference (oracle/_ref, gcc -O3 build of the reference sources) on this box's host
-    cores over the first reads of rank 0's batch: `deSAMBA classify -t nproc` (the value), the
-    same at -t 1 on a smaller sample, and read_classify(thread_num = nproc) through dlopen.
-    The -t nproc run's primary taxids are compared with the GPU's records for the same reads."""
+    cores over the first reads of rank 0's batch: `deSAMBA classify -t T` at T = the usable CPUs
+    (cgroup quota) and T = nproc, the faster being the value; -t 1 on a smaller sample; and
+    read_classify(thread_num = the faster T) through dlopen.  The value run's primary taxids are
+    compared with the GPU's records for the same reads."""
     if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "deSAMBA")):
         return None
+    import proxy_build
     cpus = host_cpus()
     nproc = cpus["nproc"]
+    eff = proxy_build.usable_cpus()
+    cpus["usable"] = eff
     sample = fastq_head(fq, n_sample)
     nb = n_bases(sample)
+    runs, sams = {}, {}
     with tempfile.TemporaryDirectory(dir=_tmp()) as d:
-        sam = os.path.join(d, "o.sam")
-        t = time.time()
-        r = _ref_classify(index_dir, sample, nproc, sam)
-        wall = time.time() - t
-        if r is None:
+        for th in sorted({eff, nproc}):
+            sam = os.path.join(d, f"o{th}.sam")
+            t = time.time()
+            r = _ref_classify(index_dir, sample, th, sam)
+            if r is None:
+                continue
+            runs[th] = {"reads": r[0], "secs": r[1], "wall_s": round(time.time() - t, 1),
+                        "value": round(r[0] / r[1], 1)}
+            sams[th] = sam
+        if not runs:
             return None
-        n, secs = r
+        best = min(runs, key=lambda th: runs[th]["secs"])
+        n, secs = runs[best]["reads"], runs[best]["secs"]
         mism = None
         if gpu_sam_sample is not None:
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             from samutil import compare
-            with open(sam, "rb") as f:
+            with open(sams[best], "rb") as f:
                 c = compare(f.read(), gpu_sam_sample)
             mism = {"reads": c["reads"], "taxid_mismatch": c["taxid_mismatch"], "mapped_mismatch": c["mapped_mismatch"],
-                    "full_record_mismatch": c["full_mismatch"]}
-    out = {"value": round(n / secs, 1), "unit": "reads/s", "cores": nproc, "kind": "reference",
-           "gbases_per_s": round(nb / secs / 1e9, 5), "host": cpus,
-           "sample": f"first {n} reads ({nb / 1e6:.1f} Mbp) of rank 0's batch, `deSAMBA classify -t {nproc}` "
-                     f"(gcc -O3 build of the reference sources), own timer {secs:.2f}s, wall {wall:.1f}s incl. index load",
+                    "full_record_mismatch": c["full_mismatch"],
+                    "note": "against the reference's -tN records (buffer pools shared across reads, SURVEY H1/H2): "
+                            "full records may differ, taxids may not"}
+    out = {"value": round(n / secs, 1), "unit": "reads/s", "cores": best, "cores_effective": eff, "nproc": nproc,
+           "kind": "reference", "gbases_per_s": round(nb / secs / 1e9, 5), "host": cpus,
+           "threads_tried": {str(th): v for th, v in runs.items()},
+           "sample": f"first {n} reads ({nb / 1e6:.1f} Mbp) of rank 0's batch, `deSAMBA classify -t {best}` "
+                     f"(gcc -O3 build of the reference sources; the faster of -t {eff} (usable CPUs) and -t {nproc} "
+                     f"(nproc)), own timer {secs:.2f}s",
            "taxid_check_vs_gpu": mism}
     s1 = fastq_head(fq, n_sample_t1)
     r1 = _ref_classify(index_dir, s1, 1, None)
     if r1:
         out["t1"] = {"value": round(r1[0] / r1[1], 1), "reads": r1[0], "secs": r1[1],
                      "gbases_per_s": round(n_bases(s1) / r1[1] / 1e9, 5)}
-    dj = _ref_dropin(index_dir, sample, nproc)
+    dj = _ref_dropin(index_dir, sample, best)
     if dj:
-        out["read_classify"] = {"value": round(n / dj["secs"], 1), "secs": dj["secs"], "thread_num": nproc,
+        out["read_classify"] = {"value": round(n / dj["secs"], 1), "secs": dj["secs"], "thread_num": best,
                                 "reads": n, "output_bytes": dj["output_bytes"]}
     return out
 
@@ -320,14 +402,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reads", type=int, default=100000, help="reads per rank")
+    ap.add_argument("--reads", type=int, default=1000000, help="reads per rank")
     ap.add_argument("--mean-len", type=int, default=8000)
-    ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS), help="proxy index (data/<w>_index.txz)")
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
+                    help="proxy index: c2 (built in the run unless data/c2_index.txz exists), c1 (data/c1_index.txz)")
     ap.add_argument("--mix", default="ont", choices=["ont", "c4"], help="ONT reads, or C4's 150 bp + 20 kb 1:1 mix")
     ap.add_argument("--index", default=None, help="index directory (overrides --workload)")
     ap.add_argument("--name", default=None, help="workload name for --index")
     ap.add_argument("--cpu-sample", type=int, default=16000, help="reads in the CPU baseline sample (-t nproc)")
     ap.add_argument("--cpu-sample-t1", type=int, default=2000, help="reads in the -t 1 CPU sample")
+    ap.add_argument("--t3-reads", type=int, default=2000, help="reads of the timed batch checked against herm_classify")
+    ap.add_argument("--dropin-reads", type=int, default=100000, help="reads in the end-to-end read_classify leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the end-to-end read_classify leg")
     ap.add_argument("--no-stats", action="store_true", help="skip the work-counter run (roofline)")
@@ -339,6 +424,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # inputs first: the index (unpacked, or the C2 proxy built) and the reads (forked workers),
+    # before this process touches a GPU
+    if a.index:
+        index_dir, workload = a.index, a.name or os.path.basename(os.path.normpath(a.index))
+    else:
+        index_dir, workload = unpack_index(rank, a.workload)
+    if a.mix == "c4":
+        workload += "+C4-mix-150bp-20kb"
+    fq = make_reads(index_dir, a.reads, 1000 + rank, a.mean_len, a.mix, world)
     import torch
     assert torch.cuda.is_available(), "bench.py needs an MI355X"
     # one process per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share devices
@@ -358,21 +452,17 @@ def main():
     import pydesamba
     import shard
 
-    if a.index:
-        index_dir, workload = a.index, a.name or os.path.basename(os.path.normpath(a.index))
-    else:
-        index_dir, workload = unpack_index(rank, a.workload)
-    if a.mix == "c4":
-        workload += "+C4-mix-150bp-20kb"
-    fq = make_reads(index_dir, a.reads, 1000 + rank, a.mean_len, a.mix)
     if dist:
         dist.barrier()
     t = time.time()
     idx = pydesamba.Index(index_dir)
     log(f"rank {rank}: index resident on cuda:{local} in {time.time() - t:.1f}s")
+    t = time.time()
     batch = idx.batch(fq)
     log(f"rank {rank}: {batch.n_reads} reads / {batch.n_bases / 1e6:.1f} Mbp resident in HBM "
-        f"(parse+upload {batch.upload['ms_h2d']:.0f} ms)")
+        f"(parse+upload {batch.upload['ms_h2d']:.0f} ms, {time.time() - t:.1f}s)")
+    # the batch holds its own copy of the text: keep only the head the CPU legs use
+    fq = fastq_head(fq, max(a.cpu_sample, a.cpu_sample_t1, a.t3_reads, a.dropin_reads))
     n_tax = idx.max_tid() + 1
     cdev = "cuda" if (dist is None or dist.get_backend() == "nccl") else "cpu"
     counts = torch.zeros(n_tax, dtype=torch.int64, device=cdev)
@@ -473,33 +563,37 @@ def main():
                 "launches_per_step": d["launches_per_step"], "avg_launch_ms": d["avg_launch_ms"], "phases": per_phase}
         stats = {"phases": ts["stats_phase"], "classB": ts["stats_B"]}
 
-    cpu = dropin = None
+    cpu = dropin = t3 = None
+    n_d = min(a.dropin_reads, batch.n_reads)
+    fq_d = fastq_head(fq, n_d)
     if rank == 0 and world == 1:
         import pydesamba as P
         n_s = min(a.cpu_sample, batch.n_reads)
         if not a.no_cpu:
+            n_t3 = min(a.t3_reads, batch.n_reads)
+            t3 = t3_check(index_dir, fastq_head(fq, n_t3), batch.format_range(0, n_t3, P.FMT_SAM))
             cpu = cpu_baseline(index_dir, fq, n_s, min(a.cpu_sample_t1, batch.n_reads),
                                batch.format_range(0, n_s, P.FMT_SAM))
         if not a.no_dropin:
-            full_sha = hashlib.sha256(batch.format(P.FMT_SAM_FULL)).hexdigest()
-            dropin = dropin_leg(idx, fq, batch.n_reads, batch.n_bases, full_sha)
+            full_sha = hashlib.sha256(batch.format_range(0, n_d, P.FMT_SAM_FULL)).hexdigest()
+            dropin = dropin_leg(idx, fq_d, n_d, n_bases(fq_d), full_sha)
     elif world > 1 and not a.no_dropin:
         # every rank: one read_classify over its own reads at the same time (after a barrier);
         # aggregate = all ranks' reads / the slowest rank's call
         import pydesamba as P
-        full_sha = hashlib.sha256(batch.format(P.FMT_SAM_FULL)).hexdigest()
+        full_sha = hashlib.sha256(batch.format_range(0, n_d, P.FMT_SAM_FULL)).hexdigest()
         dist.barrier()
-        mine = dropin_leg(idx, fq, batch.n_reads, batch.n_bases, full_sha)
+        mine = dropin_leg(idx, fq_d, n_d, n_bases(fq_d), full_sha)
         t_s = torch.tensor([mine["secs"]], dtype=torch.float64, device=cdev)
         t_ok = torch.tensor([float(mine["identical_to_batch_records"] is True)], dtype=torch.float64, device=cdev)
         dist.all_reduce(t_s, op=dist.ReduceOp.MAX)
         dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
         secs, same = float(t_s.item()), bool(t_ok.item())
         if rank == 0:
-            dropin = {"value": round(batch.n_reads * world / secs, 1), "unit": "reads/s", "secs": round(secs, 4),
-                      "reads": batch.n_reads * world, "ranks": world, "identical_to_batch_records": same,
+            dropin = {"value": round(n_d * world / secs, 1), "unit": "reads/s", "secs": round(secs, 4),
+                      "reads": n_d * world, "ranks": world, "identical_to_batch_records": same,
                       "rank0": mine,
-                      "what": "every rank: read_classify over its own 100k reads at once; slowest rank's time"}
+                      "what": f"every rank: read_classify over the first {n_d} of its reads at once; slowest rank's time"}
 
     if rank == 0:
         value = reads_total / elapsed
@@ -510,7 +604,7 @@ def main():
             "data": ("synthetic ONT reads (tools/simulate.py, lognormal mean 8 kb, 5-15% error)" if a.mix == "ont" else
                      "synthetic C4 mix (tools/simulate.py: 150 bp 1% error + ONT lognormal mean 20 kb, 1:1 interleaved)")
                     + " from a synthetic reference",
-            "config": {"workload": workload, "reads_per_rank": batch.n_reads, "mbases_per_rank": round(batch.n_bases / 1e6, 2),
+            "config": {"workload": workload, "index": index_info(index_dir), "reads_per_rank": batch.n_reads, "mbases_per_rank": round(batch.n_bases / 1e6, 2),
                        "mean_len": round(batch.n_bases / max(1, batch.n_reads)), "read_mix": a.mix, "parallelism": f"reads sharded over {world} GPU(s), index replicated",
                        "taxon_reduce": f"all_reduce({dist.get_backend()})" if world > 1 else "none"},
             "gbases_per_s": round(bases_total / elapsed / 1e9, 4),
@@ -523,6 +617,9 @@ def main():
             "cpu_baseline": cpu,
             "dropin": dropin,
         }
+        if t3:
+            line["t3_mismatch"] = t3["t3_mismatch"]
+            line["t3_check"] = t3
         if cpu:
             line["vs_cpu_baseline"] = round(value / cpu["value"], 2)
             if cpu.get("taxid_check_vs_gpu"):

@@ -68,11 +68,18 @@ int dsb_gpu_batch_counts(dsb_index *ix, dsb_gpu_batch *b, const uint32_t *weight
 
 /* The carried max_read_l of a stream of batches (the reference's one buffer pool per
  * read_classify thread, cly.c:2953): carry_in blocks until the batch before has published its
- * carry-out; carry_out publishes this batch's (called after its part A, before its part B). */
+ * carry-out; carry_out publishes this batch's (called after its part A, before its part B).
+ * A batch holds its GPU context's run lock while it waits for the carry, so the batches of one
+ * stream must take their run locks in stream order, or two streams sharing the contexts can each
+ * hold the lock the other's earlier batch needs: lock_wait (before the run lock, may block until
+ * the batch before has taken its own) and locked (right after) keep that order.  Any of the
+ * hooks may be NULL. */
 typedef struct {
 	int (*carry_in)(void *ctx);
 	void (*carry_out)(void *ctx, int carry);
 	void *ctx;
+	void (*lock_wait)(void *ctx);
+	void (*locked)(void *ctx);
 } dsb_carry_hooks;
 int dsb_gpu_batch_run_chain(dsb_index *ix, dsb_gpu_batch *b, int stats_on, const dsb_carry_hooks *hooks,
 			    dsb_gpu_timing *timing, char *err, size_t errn);

@@ -1242,7 +1242,11 @@ static int run_locked(dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stat
 	double t0 = now_ms();
 	dsb_gpu_timing T;
 	memset(&T, 0, sizeof(T));
+	if (hooks && hooks->lock_wait)
+		hooks->lock_wait(hooks->ctx);
 	pthread_mutex_lock(&g->mu);
+	if (hooks && hooks->locked)
+		hooks->locked(hooks->ctx);
 	int rc = batch_run(g, ix, b, max_read_l, stats_on, T, err, errn, hooks);
 	pthread_mutex_unlock(&g->mu);
 	T.ms_total = now_ms() - t0;

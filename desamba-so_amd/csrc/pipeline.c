@@ -54,6 +54,7 @@ typedef struct {
 	int parse_done, failed, stagers_done;
 	char err[512];
 	/* carry chain */
+	uint64_t n_locked;  /* batches that have taken their GPU run lock (they do so in input order) */
 	int carry0;
 	int *carry; uint8_t *carry_ready; uint64_t carry_cap;
 	/* output */
@@ -122,9 +123,37 @@ static int carry_in(void *ctx)
 	carry_reserve(p, c->seq);
 	while (!p->carry_ready[c->seq - 1] && !p->failed)
 		pthread_cond_wait(&p->cv, &p->mu);
-	int v = p->carry[c->seq - 1];
+	/* a failed pipeline discards every result: hand back a defined value */
+	int v = p->carry_ready[c->seq - 1] ? p->carry[c->seq - 1] : p->carry0;
 	pthread_mutex_unlock(&p->mu);
 	return v;
+}
+
+/* Run locks in input order.  A batch holds its context's run lock while it waits in carry_in for
+ * the batch before; if that batch could still be queued for a lock held by another call's waiting
+ * batch, two concurrent read_classify calls could each hold the lock the other needs.  With every
+ * call's batches taking their locks in input order, a lock holder only ever waits for an earlier
+ * batch of its own call that already holds (or has released) a lock, so the waits cannot close a
+ * cycle. */
+static void lock_wait(void *ctx)
+{
+	chain_ctx *c = ctx;
+	pipe_t *p = c->p;
+	pthread_mutex_lock(&p->mu);
+	while (p->n_locked < c->seq && !p->failed)
+		pthread_cond_wait(&p->cv, &p->mu);
+	pthread_mutex_unlock(&p->mu);
+}
+
+static void locked(void *ctx)
+{
+	chain_ctx *c = ctx;
+	pipe_t *p = c->p;
+	pthread_mutex_lock(&p->mu);
+	if (p->n_locked < c->seq + 1)
+		p->n_locked = c->seq + 1;
+	pthread_cond_broadcast(&p->cv);
+	pthread_mutex_unlock(&p->mu);
 }
 
 static void carry_out(void *ctx, int v)
@@ -230,7 +259,7 @@ static void *runner(void *arg)
 			p->runq_tail[slot] = NULL;
 		pthread_mutex_unlock(&p->mu);
 		chain_ctx cc = {p, b->seq};
-		dsb_carry_hooks h = {carry_in, carry_out, &cc};
+		dsb_carry_hooks h = {carry_in, carry_out, &cc, lock_wait, locked};
 		dsb_gpu_timing t;
 		memset(&t, 0, sizeof(t));
 		if (dsb_gpu_batch_run_chain(p->ix, b->g, p->stats_on, &h, &t, err, sizeof(err))) {

@@ -126,6 +126,41 @@ def test_concurrent_read_classify_distinct_thread_ids(gpu_index):
     assert serial[0] == golden("mixed.herm.sam_full")
 
 
+def test_concurrent_multi_batch_calls_share_contexts_without_deadlock(gpu_index):
+    """Concurrent calls that each span many GPU batches on both device contexts (DSB_PIPE_READS
+    41): every batch holds its context's run lock while it waits for the carried max_read_l of
+    the batch before, so without the in-order lock hand-out (pipeline.c lock_wait) two calls could
+    each hold the lock the other's earlier batch needs.  All calls must finish and equal the
+    serial calls."""
+    import threading
+    inputs = [golden(n + ".fq") for n in ("mixed", "ont", "illumina", "mixed")]
+    os.environ["DSB_PIPE_READS"] = "41"
+    try:
+        serial = [gpu_index.read_classify(d, thread_id=70 + k, thread_num=1) for k, d in enumerate(inputs)]
+        got = [None] * len(inputs)
+        errs = []
+
+        def work(k):
+            try:
+                for it in range(3):
+                    got[k] = gpu_index.read_classify(inputs[k], thread_id=80 + 10 * it + k, thread_num=1)
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+
+        th = [threading.Thread(target=work, args=(k,), daemon=True) for k in range(len(inputs))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=100)
+        assert not any(t.is_alive() for t in th), "concurrent read_classify calls did not finish (deadlock)"
+    finally:
+        os.environ.pop("DSB_PIPE_READS", None)
+    assert not errs
+    for k in range(len(inputs)):
+        assert got[k] == serial[k], k
+    assert serial[0] == golden("mixed.herm.sam_full")
+
+
 def test_two_calls_carry_pool_state_like_one_call(gpu_index, pyd):
     """max_read_l persists per thread_id across read_classify calls (src/cly.c:2953)."""
     fq = golden("mixed.fq")

@@ -1,15 +1,20 @@
-"""GPU parity beyond the C1 bench workload's defaults: the larger-index parameters of BASELINE
-configs C2-C4, C4's read mix, and one read_classify call spread over several GPU contexts.
+"""GPU parity beyond the fixture: the larger-index parameters of BASELINE configs C2-C4, C4's
+read mix, and one read_classify call spread over several GPU contexts.
 
-* l_ek 17 / MASK_31 / quarter-GB e-kmer tables.  The reference builder switches to them at
-  >= 238.6 M distinct 31-mers (reference src/idx.c:966-996), i.e. RefSeq-scale (C2) indexes.
-  Such an index (the 495 Mbp C2 proxy, data/c2_index.txz, 0.9 GB packed) does not fit the GPU
-  box's 512 MiB upload, so the box rebuilds the C1 proxy's tables at that size with
-  oracle/_ref/ekmer_tables, this repo's restatement of the builder's get_EXIST_kmer, which is
-  byte-identical to the builder's own l_ek-16 tables (fixture, C1) and l_ek-17 tables (C2 proxy:
-  tests/test_oracle_pinned.py, profiles/r03_c2/ekmer_check.txt).  The reference classifier
-  (oracle/_ref/herm_classify) loads that index exactly as it would a builder-made one, and is
-  the oracle on it.
+* The C2 proxy itself (tools/simulate.py preset c2: 495 Mbp, 286 M distinct 31-mers, so the
+  builder picks l_ek 17 / MASK_31; ~0.5 G BWT rows over 30 occ superblocks), built on the box by
+  tools/proxy_build.py (simulate.py + this repo's desamba_index, byte-identical to the reference
+  builder on this preset) unless DSB_C2_DIR points at one; the reference classifier
+  (oracle/_ref/herm_classify) is the oracle on it.
+* Every e-kmer table size of the reference's range (set_ekmer_par / get_EXIST_kmer, reference
+  src/idx.c:966-996; utils.h:88-95): the builder switches to larger tables as the distinct 31-mer
+  count grows (0.5 GB at >= 477 M, 1 GB at >= 954 M, 4 GB at >= 3.8 G, 16 GB at >= 15.3 G, i.e.
+  RefSeq- to nt-scale indexes).  Indexes that large cannot be built here, so the box rebuilds the
+  C1 proxy's tables at each size with oracle/_ref/ekmer_tables, this repo's restatement of the
+  builder's get_EXIST_kmer, which is byte-identical to the builder's own l_ek-16 tables (fixture,
+  C1) and l_ek-17 tables (C2 proxy: tests/test_oracle_pinned.py, profiles/r03_c2/ekmer_check.txt).
+  The reference classifier loads such an index exactly as it would a builder-made one (it reads
+  e_kmer_size from .exki and calls set_ekmer_par, idx.c:1108-1120), and is the oracle on it.
 * BASELINE C4's read mix: 150 bp Illumina-like + ONT-like reads of mean 20 kb, interleaved in a
   fixed order, after a run of short reads: the carried max_read_l (src/cly.c:2953-2963) switches
   from the Illumina rules to the long-read rule inside the input, and 20 kb+ reads take the
@@ -51,19 +56,53 @@ def c1_dir(tmp_path_factory):
     return str(d)
 
 
-@pytest.fixture(scope="module")
-def lek17_dir(c1_dir, tmp_path_factory):
-    """The C1 proxy with the quarter-GB l_ek-17 / MASK_31 e-kmer tables."""
+def _host_bytes_available():
+    """Host memory this process may still use: MemAvailable, capped by the cgroup limit."""
+    avail = None
+    with open("/proc/meminfo") as f:
+        for line in f:
+            if line.startswith("MemAvailable:"):
+                avail = int(line.split()[1]) * 1024
+    try:
+        with open("/sys/fs/cgroup/memory.max") as f:
+            v = f.read().strip()
+        if v != "max":
+            with open("/sys/fs/cgroup/memory.current") as f:
+                cur = int(f.read())
+            avail = min(avail, int(v) - cur) if avail is not None else int(v) - cur
+    except (OSError, ValueError):
+        pass
+    return avail
+
+
+def _ek_index(c1_dir, tmp_path_factory, size, l_ek):
+    """The C1 proxy with e-kmer tables of `size` bytes per table (oracle/_ref/ekmer_tables)."""
     _need(EKTAB)
-    d = tmp_path_factory.mktemp("c1_lek17")
+    need = 5 * size + (8 << 30)  # both tables written, then read by two reference runs and load_index
+    avail = _host_bytes_available()
+    if avail is not None and avail < need:
+        pytest.skip(f"host memory short for 2 x {size >> 20} MB e-kmer tables: {avail >> 30} GiB available, "
+                    f"{need >> 30} GiB needed")
+    free_disk = shutil.disk_usage(str(tmp_path_factory.getbasetemp())).free
+    if free_disk < 2 * size + (4 << 30):
+        pytest.skip(f"disk short for 2 x {size >> 20} MB e-kmer tables: {free_disk >> 30} GiB free")
+    d = tmp_path_factory.mktemp(f"c1_ek{size >> 20}M")
     for f in os.listdir(c1_dir):
         if not f.startswith("deSAMBA.exk"):
             os.symlink(os.path.join(c1_dir, f), os.path.join(d, f))
-    r = subprocess.run([EKTAB, c1_dir, str(1 << 28), str(d)], capture_output=True, text=True, check=True, timeout=300)
-    assert "l_ek 17" in r.stdout, r.stdout
+    r = subprocess.run([EKTAB, c1_dir, str(size), str(d)], capture_output=True, text=True, check=True, timeout=600)
+    assert f"l_ek {l_ek}," in r.stdout, r.stdout
     with open(os.path.join(d, "deSAMBA.exki"), "rb") as f:
-        assert int.from_bytes(f.read(8), "little") == 1 << 28
-    return str(d)
+        assert int.from_bytes(f.read(8), "little") == size
+    return d
+
+
+@pytest.fixture(scope="module")
+def lek17_dir(c1_dir, tmp_path_factory):
+    """The C1 proxy with the quarter-GB l_ek-17 / MASK_31 e-kmer tables."""
+    d = _ek_index(c1_dir, tmp_path_factory, 1 << 28, 17)
+    yield str(d)
+    shutil.rmtree(d, ignore_errors=True)
 
 
 def _sim(index_dir, tmp_path, n, seed, mix):
@@ -84,14 +123,24 @@ def _check_vs_reference(pyd, index_dir, fq, seed, tag):
     """T1 on every read, T2 on every read two reference builds agree on, T3 bounded (the
     uninitialised-memory reads of SURVEY Appendix A H1) — as tests/test_gpu_c1.py."""
     _need(HERM, GCC)
-    herm = subprocess.run([HERM, "--sam", index_dir, str(fq)], capture_output=True, check=True, timeout=900).stdout
-    t1 = subprocess.run([GCC, "--sam", "--fresh", index_dir, str(fq)], capture_output=True, check=True,
-                        timeout=900).stdout
-    idx = pyd.Index(index_dir)
+    # both reference builds run while the GPU classifies (each loads the index itself)
+    ph = subprocess.Popen([HERM, "--sam", index_dir, str(fq)], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    pg = subprocess.Popen([GCC, "--sam", "--fresh", index_dir, str(fq)], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
     try:
-        out, t, _ = idx.classify(fq.read_bytes(), fmt=1, stats=True)
+        idx = pyd.Index(index_dir)
+        try:
+            out, t, _ = idx.classify(fq.read_bytes(), fmt=1, stats=True)
+        finally:
+            idx.close()
+        herm, eh = ph.communicate(timeout=900)
+        t1, eg = pg.communicate(timeout=900)
     finally:
-        idx.close()
+        for p in (ph, pg):
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert ph.returncode == 0, eh[-400:]
+    assert pg.returncode == 0, eg[-400:]
     r = compare(herm, out)
     assert r["taxid_mismatch"] == 0 and r["mapped_mismatch"] == 0, (tag, seed, r)
     gh, gt, go = groups(herm), groups(t1), groups(out)
@@ -110,6 +159,26 @@ def test_lek17_mask31_index_matches_reference(pyd, lek17_dir, tmp_path):
     fq = _sim(lek17_dir, tmp_path, 2000, seed, "ont")
     t = _check_vs_reference(pyd, lek17_dir, fq, seed, "C1-lek17")
     assert t["seed_positions"] > 0
+
+
+# the reference's larger table sizes (src/idx.c:966-982): (bytes per table, l_ek, hash mask bits)
+EK_SIZES = [(1 << 29, 17, 32), (1 << 30, 18, 33), (1 << 32, 19, 35), (1 << 34, 20, 37)]
+
+
+@pytest.mark.parametrize("size,l_ek,mask_bits", EK_SIZES, ids=[f"lek{l}_mask{m}_{s >> 20}MB" for s, l, m in EK_SIZES])
+def test_ekmer_table_sizes_match_reference(pyd, c1_dir, tmp_path_factory, tmp_path, size, l_ek, mask_bits):
+    """l_ek 17-20 with 0.5-16 GB Bloom tables: probe offsets up to 2^37 bits (hash64_1/2 & MASK_37,
+    byte offset h >> 3 up to 2^34) against the reference classifier on the same index, T1/T2 on
+    every read and T3 bounded, on 1000 fresh reads."""
+    assert size * 8 == 1 << mask_bits
+    d = _ek_index(c1_dir, tmp_path_factory, size, l_ek)
+    try:
+        seed = int(os.environ.get("DSB_TEST_SEED", 8181 + l_ek + int.from_bytes(os.urandom(2), "little")))
+        fq = _sim(str(d), tmp_path, 1000, seed, "ont")
+        t = _check_vs_reference(pyd, str(d), fq, seed, f"C1-lek{l_ek}-mask{mask_bits}")
+        assert t["seed_positions"] > 0 or t["stats"]["ek1"] > 0
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def test_c4_mix_150bp_20kb_interleaved_matches_reference(pyd, c1_dir, tmp_path):
@@ -157,14 +226,26 @@ def test_default_two_contexts_share_one_index_copy(gpu_index, pyd):
         os.environ.pop("DSB_PIPE_READS", None)
 
 
-def test_c2_proxy_matches_reference(pyd, tmp_path):
-    """The genuine C2-direction proxy (tools/simulate.py preset c2: 495 Mbp, 286 M distinct
-    31-mers, made by the reference builder -> l_ek 17, MASK_31, 256 MB e-kmer tables, ~0.5 G BWT
-    rows over 30 occ superblocks).  Too large for the GPU box's upload, so tools/gpu_c2.sh builds
-    it on the box with oracle/_ref/deSAMBA and points DSB_C2_DIR at it; skipped elsewhere."""
+@pytest.fixture(scope="module")
+def c2_dir():
+    """The C2 proxy index: DSB_C2_DIR when set, else built here by tools/proxy_build.py
+    (simulate.py preset c2 + desamba-so_amd/bin/desamba_index, ~60 s on the GPU box's host,
+    cached under $TMPDIR for the rest of the call)."""
     d = os.environ.get("DSB_C2_DIR")
-    if not d or not os.path.exists(os.path.join(d, "deSAMBA.bwt")):
-        pytest.skip("DSB_C2_DIR not set (tools/gpu_c2.sh builds the C2 proxy on the GPU box)")
+    if d and os.path.exists(os.path.join(d, "deSAMBA.bwt")):
+        return d
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import proxy_build
+    _need(proxy_build.BUILDER)
+    return proxy_build.ensure_proxy("c2")
+
+
+def test_c2_proxy_matches_reference(pyd, c2_dir, tmp_path):
+    """The C2-direction proxy (tools/simulate.py preset c2: 495 Mbp, 286 M distinct 31-mers ->
+    l_ek 17, MASK_31, 256 MB e-kmer tables, ~0.5 G BWT rows over 30 occ superblocks): T1/T2 on
+    every read, T3 bounded, against the reference classifier on 2000 fresh ONT reads and 600
+    reads of C4's mix."""
+    d = c2_dir
     with open(os.path.join(d, "deSAMBA.exki"), "rb") as f:
         assert int.from_bytes(f.read(8), "little") == 1 << 28  # the builder chose l_ek 17 / MASK_31
     seed = int(os.environ.get("DSB_TEST_SEED", 7171 + int.from_bytes(os.urandom(2), "little")))

@@ -215,6 +215,45 @@ def simulate_c4_mix(genomes, n_reads, seed, long_mean=20000):
         yield f"m{i}_{name}", s, q
 
 
+def fastq_bytes(reads) -> bytes:
+    return b"".join(b"@" + name.encode() + b"\n" + s + b"\n+\n" + q + b"\n" for name, s, q in reads)
+
+
+_PAR = {}  # the genomes, inherited by forked workers
+
+
+def _chunk_fastq(args):
+    c, n, seed, mix, mean_len = args
+    g = _PAR["genomes"]
+    s = seed if c == 0 else seed + 7919 * c
+    gen = simulate_c4_mix(g, n, s) if mix == "c4" else simulate_reads(g, n, s, "ont", mean_len)
+    if c:
+        gen = ((f"c{c}_{name}", sq, q) for name, sq, q in gen)
+    return fastq_bytes(gen)
+
+
+def simulate_fastq_parallel(genomes, n_reads, seed, mix="ont", mean_len=8000, workers=8, chunk=10000) -> bytes:
+    """FASTQ text of n_reads reads made in chunks of `chunk` reads over forked workers: chunk 0 is
+    simulate_reads(seed) (or simulate_c4_mix) itself, chunk c > 0 the same generator seeded
+    seed + 7919 c with names prefixed `c<c>_`, so the text depends on (n_reads, seed, mix,
+    mean_len, chunk) only, never on the worker count.  Call it before the process touches a GPU
+    (the workers are forked)."""
+    import multiprocessing as mp
+    jobs = [(c, min(chunk, n_reads - c * chunk), seed, mix, mean_len) for c in range((n_reads + chunk - 1) // chunk)]
+    _PAR["genomes"] = genomes
+    try:
+        if workers <= 1 or len(jobs) <= 1:
+            parts = [_chunk_fastq(j) for j in jobs]
+        else:
+            with mp.get_context("fork").Pool(min(workers, len(jobs))) as pool:
+                parts = pool.map(_chunk_fastq, jobs, chunksize=1)
+    finally:
+        _PAR.clear()
+    out = b"".join(parts)
+    del parts
+    return out
+
+
 def write_fastq(reads, path):
     with open(path, "wb") as f:
         for name, s, q in reads:
