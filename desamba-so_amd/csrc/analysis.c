@@ -8,6 +8,10 @@
  *                                      and printed as a tree of rates   (:1898-1909, :1390-1519)
  *   ana_meta_base  <SAM> <nodes.dmp>   the same weighted by aligned read length, with mapQ
  *                                      (:1911-1922, :1684-1803)
+ *   ana_species    <SAM> <taxid> <nodes.dmp>         accuracy of every read against one true
+ *   ana_genus      <SAM> <taxid> <nodes.dmp>         taxon at species / genus rank, or at any
+ *   ana_sam        <SAM> <taxid> <nodes.dmp> <rank>  rank ("null": the true taxon is an ancestor
+ *                                      of the read's), PRIMARY and any record (:1073-1234, :2014-2025)
  *   count_base     <FASTQ>             reads and bases (:2439-2454)
  *   split_fastq    <FASTQ> <start> <step>  every step-th read from start (:2507-2532)
  *   fastq_to_fasta <FASTQ>             (:2651-2662)
@@ -168,6 +172,10 @@ static void load_rst(const char *sam_path, rst_list *L)
 		p += l;
 	}
 	free(buf);
+	if (head) { /* skip_sam_head's xassert (:343): no record line at all */
+		fprintf(stderr, "[skip_sam_head] Read SAM file FAILED\n Abort, line [344]!\n");
+		abort();
+	}
 }
 
 static int next_rst(rst_list *L, rst_t *r) /* getOneRST, :161-189 */
@@ -412,6 +420,106 @@ static int ana_meta(const char *sam, const char *nodes_dmp, int by_base)
 	return 0;
 }
 
+/* ---------------------------------------------------------------- accuracy vs one true taxon */
+/* get_tax_by_rank, :1029-1048: the first taxon at `rank` on the path to the root, or 0 */
+static uint32_t tax_by_rank(const tax_rank *tax, uint32_t t, const char *rank)
+{
+	for (uint32_t c = t;;) {
+		if (strcmp(tax[c].rank, rank) == 0)
+			return c;
+		c = tax[c].p_tid;
+		if (c <= 1 || c == NO_TID)
+			return 0;
+	}
+}
+
+/* compare_tax, :1051-1065: is `a` on the path from `b` to (below) the root */
+static int tax_is_ancestor(const tax_rank *tax, uint32_t a, uint32_t b)
+{
+	for (uint32_t c = b;;) {
+		if (c == a)
+			return 1;
+		c = tax[c].p_tid;
+		if (c <= 1 || c == NO_TID)
+			return 0;
+	}
+}
+
+static int right_classify(const tax_rank *tax, uint32_t right_tax, uint32_t tid, const char *rank, int no_rank)
+{
+	return no_rank ? tax_is_ancestor(tax, right_tax, tid) : tax_by_rank(tax, tid, rank) == right_tax;
+}
+
+/* ana_tax_des (:2014-2025) + ana_tax (:1073-1234): every read of the SAM file should come from
+ * `right_tax`; per read "\n<name> " then UM (unmapped), PRI (the primary record is right) or SEC
+ * (a later record of the read is), on stdout; the totals and rates on stderr. */
+static int ana_tax(const char *sam, uint32_t right_tax, const char *nodes_dmp, const char *rank)
+{
+	char tmp[1100];
+	snprintf(tmp, sizeof(tmp), "%s.temp", sam);
+	rst_list L;
+	load_rst(sam, &L);
+	fprintf(stderr, "%s\t", tmp);
+	int no_rank = strcmp(rank, "null") == 0;
+	tax_rank *tax;
+	load_taxonomy(nodes_dmp, &tax);
+	int wrong = 0, total = 0, unmapped = 0, right_first = 0, right_second = 0;
+	rst_t r;
+	if (next_rst(&L, &r) < 0) {
+		free(tax);
+		free(L.a);
+		return 0;
+	}
+	for (;;) {
+		total++;
+		printf("\n%s ", r.read_name);
+		if (r.isClassify == 'U') {
+			unmapped++;
+			printf("UM");
+			if (next_rst(&L, &r) < 0)
+				break;
+			continue;
+		}
+		int right = right_classify(tax, right_tax, r.tid, rank, no_rank);
+		if (right) {
+			right_first++;
+			printf("PRI");
+		}
+		char old[READ_NAME_LEN + 1];
+		strcpy(old, r.read_name);
+		int eof_ = 0;
+		for (;;) {
+			eof_ = next_rst(&L, &r);
+			if (eof_ < 0 || strcmp(old, r.read_name) != 0)
+				break;
+			if (right)
+				continue;
+			if (right_classify(tax, right_tax, r.tid, rank, no_rank)) {
+				right = 1;
+				right_second++;
+				printf("SEC");
+			}
+		}
+		if (eof_ < 0)
+			break;
+		if (!right)
+			wrong++;
+	}
+	(void)wrong;
+	fprintf(stderr, "%d\t", total);
+	fprintf(stderr, "%d\t", unmapped);
+	fprintf(stderr, "%d\t", right_first);
+	fprintf(stderr, "%d\t", right_second + right_first);
+	fprintf(stderr, "%f%%\t", (float)unmapped / total * 100);
+	fprintf(stderr, "%f%%\t", (float)right_first / total * 100);
+	fprintf(stderr, "%f%%\t", (float)right_first / (total - unmapped) * 100);
+	fprintf(stderr, "%f%%\t", (float)(right_second + right_first) / total * 100);
+	fprintf(stderr, "%f%%\n", (float)(right_second + right_first) / (total - unmapped) * 100);
+	free(tax);
+	free(L.a);
+	return 0;
+}
+
 /* ---------------------------------------------------------------- FASTQ utilities */
 static char *slurp_or_die(const char *path, uint64_t *len)
 {
@@ -482,6 +590,9 @@ static int usage(void)
 	fprintf(stderr, "usage: desamba_analysis <command> [files] [print_list]\n"
 			"  ana_meta       <SAM> <nodes.dmp>\n"
 			"  ana_meta_base  <SAM> <nodes.dmp>\n"
+			"  ana_species    <SAM> <taxid> <nodes.dmp>\n"
+			"  ana_genus      <SAM> <taxid> <nodes.dmp>\n"
+			"  ana_sam        <SAM> <taxid> <nodes.dmp> <rank|null>\n"
 			"  count_base     <FASTQ>\n"
 			"  split_fastq    <FASTQ> <start> <step>\n"
 			"  fastq_to_fasta <FASTQ>\n");
@@ -501,6 +612,12 @@ int main(int argc, char **argv)
 		return ana_meta(argv[2], argv[3], 0);
 	if (!strcmp(cmd, "ana_meta_base") && argc >= 4)
 		return ana_meta(argv[2], argv[3], 1);
+	if (!strcmp(cmd, "ana_species") && argc >= 5)
+		return ana_tax(argv[2], (uint32_t)strtoul(argv[3], NULL, 10), argv[4], "species");
+	if (!strcmp(cmd, "ana_genus") && argc >= 5)
+		return ana_tax(argv[2], (uint32_t)strtoul(argv[3], NULL, 10), argv[4], "genus");
+	if (!strcmp(cmd, "ana_sam") && argc >= 6)
+		return ana_tax(argv[2], (uint32_t)strtoul(argv[3], NULL, 10), argv[4], argv[5]);
 	if (!strcmp(cmd, "count_base") && argc >= 3)
 		return count_base(argv[2]);
 	if (!strcmp(cmd, "split_fastq") && argc >= 5) {
