@@ -136,6 +136,11 @@ void dsb_str_printf(dsb_str *s, const char *fmt, ...);
 enum { DSB_OUT_SAM = 1, DSB_OUT_SAM_FULL = 2, DSB_OUT_DES = 3, DSB_OUT_DES_FULL = 4 };
 void dsb_format_read(dsb_str *out, const dsb_index *ix, const dsb_reads_t *r, uint64_t i,
 		     const dsb_read_out_t *ro, const dsb_hit_out_t *hits, int format, int max_sec_N);
+void dsb_sam_seq_qual(const dsb_rec_t *rec, const char **seq, uint64_t *seq_n, const char **qual, uint64_t *qual_n);
+/* the same records; SAM_FULL with hole != NULL leaves out "SEQ\tQUAL" (*hole_n bytes) and sets
+ * *hole to the offset in out where they go (*hole = UINT64_MAX: no hole) */
+void dsb_format_read_hole(dsb_str *out, const dsb_index *ix, const dsb_reads_t *r, uint64_t i, const dsb_read_out_t *ro,
+			  const dsb_hit_out_t *hits, int format, int max_sec_N, uint64_t *hole, uint64_t *hole_n);
 /* printed length of a %s argument held as (p, n): up to the first NUL */
 static inline uint64_t dsb_cstr_len(const char *p, uint64_t n) { return p ? strnlen(p, n) : 0; }
 

@@ -107,6 +107,7 @@ typedef struct {
 	uint64_t *lds_key;      /* wave chaining: anchor sort keys / ids in LDS (DSB_SORT_LDS entries), or 0 */
 	uint32_t *lds_id;
 	uint16_t *lds_cand;     /* wave scoring: 64 candidate slots of the register k-mer match (DSB_MATCH_BF), or 0 */
+	uint8_t *lds_q;         /* wave scoring: DSB_QCOPY_BYTES of LDS for a window's read range (DSB_QCOPY), or 0 */
 	uint8_t *lds_hb;        /* wave read-hash build: DSB_HB_LDS lane-id bytes in LDS (key groups of a chunk), or 0 */
 	uint32_t *hh[2], *hn[2]; /* read 9-mer hash per strand: list heads per key, one node per position */
 	dsb_sch_t *sch;         /* 256 + 2*400 */
@@ -460,6 +461,68 @@ DSB_HD int dsb_isl_step(dsb_isl_t *s, uint32_t mb, uint32_t *so, uint32_t *sl)
 	}
 	s->mode = (s->fwd ? s->i < s->nk : s->i >= 0) ? DSB_ISL_GRID : DSB_ISL_DONE;
 	return 1;
+}
+
+/* Exist bits the scan has already probed, in a 64-position window of the strand (k_island_g,
+ * DSB_ISL_MEMO): a grid batch probes positions past the first hit, and a run batch past the end
+ * of the run; the batches after them (the hit's run, the grid after the seed) meet some of those
+ * positions again, and take their bits from here instead of probing the tables again (tools/
+ * island_sim.py: 0.64 -> 0.54 probes per position at grid 8 / run 16 on the C2 proxy).  Same bits,
+ * so the same seeds (tests/emu/isl_check.cpp checks every memo bit against the true bit). */
+typedef struct {
+	int32_t kb;            /* window: positions [kb, kb + 64) */
+	uint64_t known, val;   /* bit q - kb: probed / its exist bit */
+} dsb_isl_memo_t;
+
+DSB_HD void dsb_isl_memo_init(dsb_isl_memo_t *m)
+{
+	m->kb = 0;
+	m->known = m->val = 0;
+}
+
+/* move the window so that it holds positions [lo, hi] (hi - lo < 64): forward scans only move up,
+ * reverse scans down, so the bits dropped are behind the scan */
+DSB_HD void dsb_isl_memo_cover(dsb_isl_memo_t *m, int fwd, int lo, int hi)
+{
+	if (lo > hi || (lo >= m->kb && hi < m->kb + 64))
+		return;
+	int nkb = fwd ? lo : hi - 63;
+	int sh = nkb - m->kb;
+	if (sh >= 64 || sh <= -64) {
+		m->known = m->val = 0;
+	} else if (sh > 0) {
+		m->known >>= sh;
+		m->val >>= sh;
+	} else if (sh < 0) {
+		m->known <<= -sh;
+		m->val <<= -sh;
+	}
+	m->kb = nkb;
+}
+
+/* the exist bit of position q when the window holds it */
+DSB_HD int dsb_isl_memo_get(const dsb_isl_memo_t *m, int q, int *b)
+{
+	uint32_t o = (uint32_t)(q - m->kb);
+	if (q < 0 || o >= 64 || !((m->known >> o) & 1))
+		return 0;
+	*b = (int)((m->val >> o) & 1);
+	return 1;
+}
+
+/* record a batch's bits (state s before dsb_isl_step; bit g of mb = position dsb_isl_pos(s, g)) */
+template <int GG, int GR>
+DSB_HD void dsb_isl_memo_put(dsb_isl_memo_t *m, const dsb_isl_t *s, uint32_t mb)
+{
+	int G = GG > GR ? GG : GR;
+	for (int g = 0; g < G; g++) {
+		int q = dsb_isl_pos<GG, GR>(s, g);
+		uint32_t o = (uint32_t)(q - m->kb);
+		if (q >= 0 && o < 64) {
+			m->known |= 1ull << o;
+			m->val = (m->val & ~(1ull << o)) | ((uint64_t)((mb >> g) & 1) << o);
+		}
+	}
 }
 
 /* get_seed_vector_M2's top-seed pass (src/cly.c:1190-1225) over seeds as they are produced: after
@@ -2987,6 +3050,46 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 			}
 		}
 #endif
+#ifndef DSB_QCOPY
+#define DSB_QCOPY 0
+#endif
+#define DSB_BIN_TAIL_BYTES 256 /* bytes after R in the read buffer (dsb_ws.h DSB_BIN_TAIL) */
+#ifndef DSB_QCOPY_BYTES
+#define DSB_QCOPY_BYTES 768
+#endif
+		/* The candidates' extensions (MEM_search over the read bytes) read the window's read
+		 * range [q_bg, q_ed] and a few bytes around it.  With DSB_QCOPY, when that range fits, the
+		 * wave copies it once into LDS (one coalesced load per lane), and an extension whose bytes
+		 * all lie inside the copy reads LDS instead of making its own dependent global round
+		 * trips; the others read the read buffer.  Same bytes either way.  The LDS address is
+		 * always formed as lds_q + (x - qv_lo) with 0 <= x - qv_lo < DSB_QCOPY_BYTES, never as an
+		 * LDS pointer moved outside the array and indexed back in (round 3's version of this
+		 * copy did that: an LDS pointer is a 32-bit offset, so lds_q - (qca - q_str) wrapped, and
+		 * converted to a flat address then offset by 64-bit arithmetic it pointed outside the
+		 * shared aperture - a memory violation on the box). */
+		int64_t qv_lo = 1, qv_hi = 0; /* read bytes [qv_lo, qv_hi] are in LDS at lds_q[x - qv_lo] */
+#if DSB_QCOPY
+		{
+			/* the copy stays inside the read buffer (the F | R halves + the tail guard) */
+			const uint8_t *qca = (const uint8_t *)((uintptr_t)(q_str + q_bg - 32) & ~(uintptr_t)7);
+			if (w->lds_q && q_bg <= q_ed && (int64_t)q_ed - (int64_t)q_bg + 128 <= DSB_QCOPY_BYTES - 16 &&
+			    (int64_t)q_bg >= 32 && qca >= w->bin && qca + DSB_QCOPY_BYTES <= w->bin + 2ull * w->L + DSB_BIN_TAIL_BYTES) {
+				const uint64_t *src = (const uint64_t *)qca;
+				uint64_t *dst = (uint64_t *)w->lds_q;
+				for (uint32_t k = lane; k < DSB_QCOPY_BYTES / 8; k += DSB_WV)
+					dst[k] = src[k];
+				dsb_wsync();
+				qv_lo = (int64_t)(qca - q_str);
+				qv_hi = qv_lo + DSB_QCOPY_BYTES - 1;
+			}
+		}
+#endif
+		/* read byte x of the strand for an access touching bytes [a, b] */
+		auto qat = [&](int64_t x, int64_t a, int64_t b) -> const uint8_t * {
+			if (DSB_QCOPY && a >= qv_lo && b <= qv_hi)
+				return w->lds_q + (x - qv_lo);
+			return q_str + x;
+		};
 		/* software pipeline: the next batch's probe and list head are loaded before this
 		 * batch's lists are walked, so that their latency overlaps the walk */
 		const uint8_t *n_cts = t_str;
@@ -3052,13 +3155,14 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 					if (w->stats) w->stats[DSB_ST_NCAND]++;
 					dsb_spd_t e;
 					int ok = 0;
+					int64_t xb = (int64_t)q_pos - 1, xf = (int64_t)q_pos + DSB_S_A_KMER_L;
 					if (isForward) {
-						int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, 4);
+						int back_len = dsb_MEM_search(qat(xb, xb - 24, xb + 16), c_t_str - 1, 0, 4);
 						if (back_len < 4 || i == 4) {
 							uint32_t max_search = q_ed - q_pos - 1;
 							max_search = DSB_MIN(max_search, t_len - i - 1) + DSB_OVER_SEARCH;
-							int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L,
-											 1, (int)max_search);
+							int forward_len = dsb_MEM_search(qat(xf, xf - 8, xf + (int64_t)max_search + 16),
+											 c_t_str + DSB_S_A_KMER_L, 1, (int)max_search);
 							int total_len = back_len + forward_len + 1;
 							if (total_len >= 4) {
 								e.len = total_len;
@@ -3068,11 +3172,12 @@ DSB_HDN void dsb_sdp_match_impl(dsb_read_ws *w, uint32_t q_bg, uint32_t q_ed, co
 							}
 						}
 					} else {
-						int forward_len = dsb_MEM_search(q_str + q_pos + DSB_S_A_KMER_L, c_t_str + DSB_S_A_KMER_L, 1, 4);
+						int forward_len = dsb_MEM_search(qat(xf, xf - 8, xf + 20), c_t_str + DSB_S_A_KMER_L, 1, 4);
 						if (forward_len < 4 || i == 4) {
 							uint32_t max_search = q_pos;
 							max_search = DSB_MIN(max_search, (uint32_t)(c_t_str - t_str)) + DSB_OVER_SEARCH;
-							int back_len = dsb_MEM_search(q_str + q_pos - 1, c_t_str - 1, 0, (int)max_search);
+							int back_len = dsb_MEM_search(qat(xb, xb - (int64_t)max_search - 24, xb + 16), c_t_str - 1, 0,
+										      (int)max_search);
 							int total_len = back_len + forward_len + 1;
 							if (total_len >= 4) {
 								e.len = total_len;

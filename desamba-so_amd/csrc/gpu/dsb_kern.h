@@ -188,6 +188,9 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 #ifndef DSB_ISL_GR
 #define DSB_ISL_GR 0 /* positions per run batch (0: DSB_ISLAND_G) */
 #endif
+#ifndef DSB_ISL_MEMO
+#define DSB_ISL_MEMO 0 /* reuse the bits of positions an earlier batch probed (dsb_isl_memo_t) */
+#endif
 template <int G, int STATS>
 __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 								   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
@@ -237,6 +240,8 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 			break;
 		dsb_isl_t s;
 		dsb_isl_init(&s, nk, strand == 0, mine);
+		dsb_isl_memo_t memo;
+		dsb_isl_memo_init(&memo);
 		if (mine)
 			dsb_top_init(&top);
 		for (;;) {
@@ -251,6 +256,8 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 			 * when the batch leaves it; each k-mer's four words come by lane shuffles */
 			int lo, hi;
 			dsb_isl_span<GG, GR>(&s, &lo, &hi);
+			if (DSB_ISL_MEMO && s.mode != DSB_ISL_DONE)
+				dsb_isl_memo_cover(&memo, s.fwd, lo, hi);
 			int64_t klo = ((int64_t)lo + bo) >> 3, khi = (((int64_t)hi + bo) >> 3) + 3;
 			if (s.mode != DSB_ISL_DONE && lo <= hi && (klo < wb || khi >= wb + G)) {
 				wb = s.fwd ? klo : DSB_MAX(khi - (G - 1), wmin);
@@ -275,7 +282,9 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 				uint64_t km = dsb_kmer_at(bin + q, l_ek, sbm);
 #endif
 				pv = (uint32_t)(km & DSB_PRE_IDX_MASK);
-				if (km) {
+				if (DSB_ISL_MEMO && dsb_isl_memo_get(&memo, q, &b)) {
+					/* probed by an earlier batch */
+				} else if (km) {
 					uint64_t h1 = dsb_hash64_1(km) & ix->ek_mask;
 					p1++;
 					if ((dsb_gld(ix->ek0 + (h1 >> 3)) >> (7 - (h1 & 0x7))) & 0x1) {
@@ -288,6 +297,8 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 			uint32_t mb = (uint32_t)(__ballot(b) >> (sg * G)) & GM;
 			if (q >= 0 && (s.mode != DSB_ISL_GRID || (mb && (int)gl == __builtin_ctz(mb))))
 				pre[q] = pv;
+			if (DSB_ISL_MEMO)
+				dsb_isl_memo_put<GG, GR>(&memo, &s, mb);
 			uint32_t so = 0, sl = 0;
 			if (dsb_isl_step<GG, GR>(&s, mb, &so, &sl) && gl == 0) {
 				uint32_t m = top.n, ti;
@@ -414,6 +425,12 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 			static_assert(DSB_WIN_LDS_BYTES <= DSB_DELA_CAND_OFF && DSB_DELA_CAND_OFF + 128 <= DSB_DELA_LDS_BYTES,
 				      "candidate slots must not overlap the windows");
 			w.lds_cand = (uint16_t *)((uint8_t *)dela_lds + DSB_DELA_CAND_OFF);
+			/* a window's read range (DSB_QCOPY): the LDS past the windows */
+			static_assert(!DSB_QCOPY || (DSB_WIN_LDS_BYTES + DSB_QCOPY_BYTES <= DSB_DELA_LDS_BYTES && (DSB_WIN_LDS_BYTES & 7) == 0),
+				      "the read-range copy must fit past the windows");
+			static_assert(!(DSB_MATCH_BF && DSB_QCOPY), "the candidate slots share the read-range copy's LDS");
+			if (DSB_QCOPY)
+				w.lds_q = (uint8_t *)dela_lds + DSB_WIN_LDS_BYTES;
 			dsb_phase<true>(&w, &f, ph);
 		} else
 			dsb_phase<true>(&w, &f, ph);

@@ -12,6 +12,7 @@
 
 #define DSB_BIN_GUARD 64   /* bytes before F: the last 8 = glibc chunk header of the reference buffer */
 #define DSB_BIN_TAIL 256   /* bytes after R, MALLOC_PERTURB fill */
+static_assert(DSB_BIN_TAIL == DSB_BIN_TAIL_BYTES, "the scoring's read-range copy bound (dsb_classify.h)");
 #define DSB_STATE_BYTES 128
 #define DSB_CAP_RETRY 8
 #define DSB_SCALE_UNIT 8   /* capacity scale is fixed point: DSB_SCALE_UNIT = the default capacities */
@@ -94,6 +95,7 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 	w->lds_id = 0;
 	w->lds_hb = 0;
 	w->lds_cand = 0;
+	w->lds_q = 0;
 	uint32_t *h = (uint32_t *)(base + o.hash);
 	uint64_t hs = 1ull << o.kl;
 	for (int s = 0; s < 2; s++) {

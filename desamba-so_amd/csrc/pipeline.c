@@ -59,8 +59,10 @@ typedef struct {
 	int *carry; uint8_t *carry_ready; uint64_t carry_cap;
 	/* output */
 	char *out; uint64_t out_n, out_m;
-	/* formatter per-task buffers */
+	/* formatter per-task buffers; SAM_FULL: per read the offset in its task buffer where SEQ\tQUAL
+	 * go (composed straight into the output by the copy pass), per task the output bytes */
 	dsb_str *tbuf; uint64_t n_tbuf;
+	uint64_t *hole, hole_cap, *tsize;
 	/* accounting */
 	dsb_gpu_timing gt;
 	double ms_parse, ms_gather, ms_format, ms_wait_gpu;
@@ -304,17 +306,47 @@ static void format_task(void *c_, uint64_t t, int worker)
 		hi = c->b->reads.n;
 	const dsb_read_out_t *ro = dsb_gpu_batch_ro(c->b->g);
 	const dsb_hit_out_t *hits = dsb_gpu_batch_hits(c->b->g);
-	for (uint64_t i = lo; i < hi; i++)
-		dsb_format_read(s, p->ix, &c->b->reads, i, ro + i, hits + ro[i].hit_off, p->format, p->max_sec_N);
+	uint64_t extra = 0;
+	for (uint64_t i = lo; i < hi; i++) {
+		uint64_t hn = 0;
+		dsb_format_read_hole(s, p->ix, &c->b->reads, i, ro + i, hits + ro[i].hit_off, p->format, p->max_sec_N,
+				     p->hole + i, &hn);
+		if (p->hole[i] != UINT64_MAX)
+			extra += hn;
+	}
+	p->tsize[t] = s->l + extra;
 }
 
+/* the task's records into the output: its buffer, with each read's SEQ\tQUAL copied from the
+ * record views into the holes (SAM_FULL) */
 static void copy_task(void *c_, uint64_t t, int worker)
 {
 	(void)worker;
 	fmt_ctx *c = c_;
 	pipe_t *p = c->p;
-	if (p->tbuf[t].l)
-		memcpy(p->out + c->off[t], p->tbuf[t].s, p->tbuf[t].l);
+	const dsb_str *s = p->tbuf + t;
+	char *d = p->out + c->off[t];
+	uint64_t lo = t * c->per_task, hi = lo + c->per_task, pos = 0;
+	if (hi > c->b->reads.n)
+		hi = c->b->reads.n;
+	for (uint64_t i = lo; i < hi; i++) {
+		uint64_t h = p->hole[i];
+		if (h == UINT64_MAX)
+			continue;
+		memcpy(d, s->s + pos, h - pos);
+		d += h - pos;
+		pos = h;
+		const char *sq, *ql;
+		uint64_t sn, qn;
+		dsb_sam_seq_qual(c->b->reads.rec + i, &sq, &sn, &ql, &qn);
+		memcpy(d, sq, sn);
+		d += sn;
+		*d++ = '\t';
+		memcpy(d, ql, qn);
+		d += qn;
+	}
+	if (s->l > pos)
+		memcpy(d, s->s + pos, s->l - pos);
 }
 
 static int format_batch(pipe_t *p, pbatch *b)
@@ -330,14 +362,19 @@ static int format_batch(pipe_t *p, pbatch *b)
 	if (n_tasks > p->n_tbuf) {
 		p->tbuf = realloc(p->tbuf, n_tasks * sizeof(dsb_str));
 		memset(p->tbuf + p->n_tbuf, 0, (n_tasks - p->n_tbuf) * sizeof(dsb_str));
+		p->tsize = realloc(p->tsize, n_tasks * sizeof(uint64_t));
 		p->n_tbuf = n_tasks;
+	}
+	if (n > p->hole_cap) {
+		p->hole = realloc(p->hole, n * sizeof(uint64_t));
+		p->hole_cap = n;
 	}
 	dsb_pool_run(p->pool, n_tasks, format_task, &c);
 	uint64_t *off = malloc((n_tasks + 1) * sizeof(uint64_t));
 	uint64_t tot = p->out_n;
 	for (uint64_t t = 0; t < n_tasks; t++) {
 		off[t] = tot;
-		tot += p->tbuf[t].l;
+		tot += p->tsize[t];
 	}
 	if (tot + 1 > p->out_m) { /* large chunks are mmap'd: realloc moves pages, not bytes */
 		uint64_t m = p->out_m ? p->out_m : (1u << 20);
@@ -553,6 +590,8 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 	for (uint64_t t = 0; t < p->n_tbuf; t++)
 		free(p->tbuf[t].s);
 	free(p->tbuf);
+	free(p->tsize);
+	free(p->hole);
 	free(p->by_seq);
 	free(p->carry);
 	free(p->carry_ready);

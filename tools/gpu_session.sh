@@ -1,0 +1,65 @@
+#!/bin/bash
+# tools/gpu_session.sh TAG STEP... — one GPU call made of named steps, each under its own time
+# limit, outputs under gpurun_out/TAG/; the call stops at the first failing step.
+#
+#   bench[:ARGS]      python bench.py ARGS (default: the driver's defaults, 5 steps)   -> bench.json
+#   ab:VARS:ARGS      bench.py --no-cpu --no-stats --no-dropin ARGS for the default library and
+#                     each desamba-so_amd/lib/var_VAR.so (VARS comma-separated)         -> ab_*.json
+#   parity:VAR        tests/test_gpu_parity.py + test_gpu_c1.py with lib/var_VAR.so     -> parity_VAR.log
+#   scale[:K]         tests/test_gpu_scale.py -k K (C2 proxy, e-kmer table sizes)       -> scale.log
+#   suite             the whole -m gpu suite                                            -> suite.log
+#   prof[:ARGS]       rocprofv3 --kernel-trace --stats over bench.py ARGS               -> prof/
+#   pmc:COUNTERS:ARGS one rocprofv3 --pmc pass over bench.py ARGS                        -> pmc_N/
+#
+# Usage: gpurun -- 'bash tools/gpu_session.sh r4a bench ab:qcopy,memo:--reads=300000 scale'
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+TAG=$1; shift
+O=gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=${TMPDIR:-/tmp}
+{ date; df -h /tmp "$TMPDIR" /dev/shm; free -g; cat /sys/fs/cgroup/memory.max /sys/fs/cgroup/cpu.max; nproc; } > "$O/env.txt" 2>&1
+PY="python -u"
+npmc=0
+for step in "$@"; do
+	name=${step%%:*}
+	rest=${step#*:}; [ "$rest" = "$step" ] && rest=""
+	echo "[gpu_session] $(date +%T) $step" | tee -a "$O/steps.txt"
+	case $name in
+	bench)
+		timeout -k 10 560 $PY bench.py ${rest:---steps 5 --warmup 1} > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
+		tail -c 600 "$O/bench.json" ;;
+	ab)
+		vars=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+		args=${args//=/ }
+		for v in base ${vars//,/ }; do
+			if [ "$v" = base ]; then unset DSB_LIB; else export DSB_LIB=desamba-so_amd/lib/var_$v.so; fi
+			timeout -k 10 300 $PY bench.py --no-cpu --no-stats --no-dropin $args > "$O/ab_$v.json" 2> "$O/ab_$v.err" || { tail -20 "$O/ab_$v.err"; exit 1; }
+			python3 -c "import json; d=json.load(open('$O/ab_$v.json')); print('$v', d['value'], d['ms_per_step'], {k: round(x, 1) for k, x in d['phase_ms_classA'].items()})" | tee -a "$O/ab.txt"
+		done
+		unset DSB_LIB ;;
+	parity)
+		DSB_LIB=desamba-so_amd/lib/var_$rest.so timeout -k 10 400 $PY -m pytest tests/test_gpu_parity.py tests/test_gpu_c1.py -x -q --timeout 300 --timeout-method thread > "$O/parity_$rest.log" 2>&1 || { tail -30 "$O/parity_$rest.log"; exit 1; }
+		tail -2 "$O/parity_$rest.log" ;;
+	scale)
+		timeout -k 10 900 $PY -m pytest tests/test_gpu_scale.py -x -v -s ${rest:+-k "$rest"} --timeout 600 --timeout-method thread > "$O/scale.log" 2>&1 || { tail -40 "$O/scale.log"; exit 1; }
+		grep -E "PASSED|FAILED|SKIPPED|T3 mismatches" "$O/scale.log" | tail -20 ;;
+	suite)
+		timeout -k 10 1000 $PY -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > "$O/suite.log" 2>&1 || { tail -40 "$O/suite.log"; exit 1; }
+		tail -3 "$O/suite.log" ;;
+	prof)
+		rm -rf "$O/prof"
+		timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py ${rest:---steps 3 --warmup 1 --no-cpu --no-dropin} > "$O/prof_bench.json" 2> "$O/prof.err" || { tail -20 "$O/prof.err"; exit 1; }
+		find "$O/prof" -name "*kernel_stats.csv" | head -1 | xargs -r head -12 ;;
+	pmc)
+		ctr=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
+		args=${args//=/ }
+		npmc=$((npmc + 1))
+		rm -rf "$O/pmc_$npmc"
+		timeout -s KILL 400 rocprofv3 --pmc ${ctr//,/ } -d "$O/pmc_$npmc" -o run -- python3 bench.py ${args:---steps 1 --warmup 0 --no-cpu --no-dropin --no-stats} > "$O/pmc_$npmc.json" 2> "$O/pmc_$npmc.err" || { tail -20 "$O/pmc_$npmc.err"; exit 1; }
+		echo "$ctr" > "$O/pmc_$npmc/counters.txt" ;;
+	*)
+		echo "unknown step $step"; exit 2 ;;
+	esac
+done
+echo "[gpu_session] $(date +%T) done" | tee -a "$O/steps.txt"
