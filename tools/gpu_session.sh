@@ -4,7 +4,9 @@
 #
 #   bench[:ARGS]      python bench.py ARGS (default: the driver's defaults, 5 steps)   -> bench.json
 #   ab:VARS:ARGS      bench.py --no-cpu --no-stats --no-dropin ARGS for the default library and
-#                     each desamba-so_amd/lib/var_VAR.so (VARS comma-separated)         -> ab_*.json
+#                     each variant (VARS comma-separated): desamba-so_amd/lib/var_VAR.so, or
+#                     env.KEY.VALUE = the default library with KEY=VALUE (DROPIN= keeps the
+#                     drop-in leg)                                                     -> ab_*.json
 #   parity:VAR        tests/test_gpu_parity.py + test_gpu_c1.py with lib/var_VAR.so     -> parity_VAR.log
 #   scale[:K]         tests/test_gpu_scale.py -k K (C2 proxy, e-kmer table sizes)       -> scale.log
 #   suite             the whole -m gpu suite                                            -> suite.log
@@ -27,15 +29,21 @@ for step in "$@"; do
 	echo "[gpu_session] $(date +%T) $step" | tee -a "$O/steps.txt"
 	case $name in
 	bench)
+		rest=${rest//=/ }
 		timeout -k 10 560 $PY bench.py ${rest:---steps 5 --warmup 1} > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
 		tail -c 600 "$O/bench.json" ;;
-	ab)
+	ab|abd) # abd: with the drop-in leg
+		[ "$name" = abd ] && DROPIN="" || unset DROPIN
 		vars=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""
 		args=${args//=/ }
 		for v in base ${vars//,/ }; do
-			if [ "$v" = base ]; then unset DSB_LIB; else export DSB_LIB=desamba-so_amd/lib/var_$v.so; fi
-			timeout -k 10 300 $PY bench.py --no-cpu --no-stats --no-dropin $args > "$O/ab_$v.json" 2> "$O/ab_$v.err" || { tail -20 "$O/ab_$v.err"; exit 1; }
-			python3 -c "import json; d=json.load(open('$O/ab_$v.json')); print('$v', d['value'], d['ms_per_step'], {k: round(x, 1) for k, x in d['phase_ms_classA'].items()})" | tee -a "$O/ab.txt"
+			# a variant is lib/var_V.so, or env.KEY.VALUE (the default library with KEY=VALUE)
+			envs=()
+			if [ "$v" = base ]; then unset DSB_LIB
+			elif [[ $v == env.* ]]; then unset DSB_LIB; kv=${v#env.}; envs=("${kv%%.*}=${kv#*.}")
+			else export DSB_LIB=desamba-so_amd/lib/var_$v.so; fi
+			env "${envs[@]}" timeout -k 10 300 $PY bench.py --no-cpu --no-stats ${DROPIN---no-dropin} $args > "$O/${name}_$v.json" 2> "$O/${name}_$v.err" || { tail -20 "$O/${name}_$v.err"; exit 1; }
+			python3 -c "import json; d=json.load(open('$O/${name}_$v.json')); print('$v', d['value'], d['ms_per_step'], {k: round(x, 1) for k, x in d['phase_ms_classA'].items()}, 'dropin', (d.get('dropin') or {}).get('value'), (d.get('dropin') or {}).get('identical_to_batch_records'))" | tee -a "$O/$name.txt"
 		done
 		unset DSB_LIB ;;
 	parity)
@@ -48,6 +56,7 @@ for step in "$@"; do
 		timeout -k 10 1000 $PY -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > "$O/suite.log" 2>&1 || { tail -40 "$O/suite.log"; exit 1; }
 		tail -3 "$O/suite.log" ;;
 	prof)
+		rest=${rest//=/ }
 		rm -rf "$O/prof"
 		timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py ${rest:---steps 3 --warmup 1 --no-cpu --no-dropin} > "$O/prof_bench.json" 2> "$O/prof.err" || { tail -20 "$O/prof.err"; exit 1; }
 		find "$O/prof" -name "*kernel_stats.csv" | head -1 | xargs -r head -12 ;;
