@@ -770,15 +770,20 @@ static int pipe_halves(void)
 	return v;
 }
 
-/* The split of part A (run_split) is off by default: with the slow reads' seeds no longer
- * replayed serially, the slow phases take ~9 ms in a row, while beside the scoring grid their
- * workgroups wait for its waves to free CUs (measured r02: 564k vs 555k reads/s).  DSB_SPLIT=1
- * turns it on. */
+/* The split of part A (run_split): after resolve_f the reads that still need slow seeding run
+ * their slow phases on the library stream while the scoring of every other read runs on the
+ * second stream.  On by default since round 4: on the C2 proxy the slow phases are ~14% of a step
+ * (slow0 21 ms per 111k-read chunk, a few thousand long-running waves that leave most CUs idle),
+ * and beside the scoring grid they cost little: 543.8k -> 579.7k reads/s (C2, 300k reads, one
+ * box, profiles/r04_b).  On the C1 proxy of round 2 (slow phases ~9 ms of 160) it measured 555k
+ * vs 564k without.  DSB_SPLIT=0 turns it off. */
 static int split_slow(void)
 {
 	static int v = -1;
-	if (v < 0)
-		v = getenv("DSB_SPLIT") ? 1 : 0;
+	if (v < 0) {
+		const char *e = getenv("DSB_SPLIT");
+		v = e ? (atoi(e) != 0) : 1;
+	}
 	return v;
 }
 
@@ -835,9 +840,27 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 	return 1;
 }
 
+/* DSB_HOST_TIMING=1 (diagnostic): per batch_run, the host wall time of each section of the chunk
+ * loop on stderr (the GPU idles in the sections that end in a synchronisation) */
+enum { HS_SIZE, HS_SETUP, HS_PARTA, HS_SYNC_A, HS_RETRY, HS_CARRY_B, HS_D2H, HS_N };
+static const char *hs_name[HS_N] = {"size", "setup", "partA_launch", "sync_A+ro", "retry", "carry+classB", "d2h"};
+static int host_timing(void)
+{
+	static int v = -1;
+	if (v < 0)
+		v = getenv("DSB_HOST_TIMING") ? 1 : 0;
+	return v;
+}
+
 static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on,
 		     dsb_gpu_timing &T, char *err, size_t errn, const dsb_carry_hooks *hooks = nullptr)
 {
+	double hs[HS_N] = {0}, hs_t = now_ms();
+	auto hs_mark = [&](int k) {
+		double t = now_ms();
+		hs[k] += t - hs_t;
+		hs_t = t;
+	};
 	HIP_OK(hipSetDevice(g->device));
 	hipStream_t s = g->stream;
 	if (b->up_pending) { /* a streamed batch: its bases are still on the way on the copy stream */
@@ -888,6 +911,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	size_t budget = ws_budget(g, hooks ? g->n_ctx : 1);
 	int carry = *max_read_l;
 	int l_ek = ix->l_ek;
+	hs_mark(HS_SETUP);
 	for (uint64_t cb = 0; cb < n;) {
 		/* ---- chunk [cb, ce) within the workspace budget, input order */
 		uint64_t ce = cb, ws_total = 0;
@@ -901,6 +925,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		}
 		uint32_t cn = (uint32_t)(ce - cb);
 		T.n_chunks++;
+		hs_mark(HS_SIZE);
 		uint64_t rused = 0; /* bytes of the retry buffer holding this chunk's re-run reads */
 		void *ws_before = g->ws.p;
 		if (g->ws.ensure(ws_total + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
@@ -916,6 +941,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		const std::vector<uint32_t> &order = chunk_order(b, cb, ce);
 		HIP_OK(hipMemcpyAsync(g->order.p, order.data(), 4ull * cn, hipMemcpyHostToDevice, s));
 		uint8_t *wsb = g->ws.as<uint8_t>();
+		hs_mark(HS_SETUP);
 		hipEventRecord(g->ev_a, s);
 		k_encode<<<cn, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, nullptr, cn);
 		T.ms_encode += ev_ms(g);
@@ -1046,10 +1072,12 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			}
 		}
 		HIP_OK(hipGetLastError());
+		hs_mark(HS_PARTA);
 		HIP_OK(hipStreamSynchronize(s));
 		uint32_t n_over = 0;
 		HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
 		HIP_OK(hipMemcpy(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
+		hs_mark(HS_SYNC_A);
 		/* ---- overflow: re-run those reads with 8x capacities in extra workspace */
 		while (n_over) {
 			std::vector<uint32_t> sel;
@@ -1119,6 +1147,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
 			HIP_OK(hipMemcpy(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
 		}
+		hs_mark(HS_RETRY);
 		if (getenv("DSB_DEBUG_READ")) { /* diagnostic: dump one read's workspace after stage A */
 			uint64_t dr = strtoull(getenv("DSB_DEBUG_READ"), NULL, 10);
 			if (dr >= cb && dr < ce) {
@@ -1168,6 +1197,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 							 b->d_tid.as<uint32_t>() + cb, g->stats.as<unsigned long long>());
 		T.ms_classB += ev_ms(g);
 		HIP_OK(hipGetLastError());
+		hs_mark(HS_CARRY_B);
 		double td = now_ms();
 		uint32_t nh = 0;
 		HIP_OK(hipMemcpy(&nh, g->cnt.p, 4, hipMemcpyDeviceToHost));
@@ -1180,7 +1210,14 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		for (uint32_t i = 0; i < cn; i++)
 			ro[cb + i].hit_off = base + hit_off[cb + i];
 		T.ms_d2h += now_ms() - td;
+		hs_mark(HS_D2H);
 		cb = ce;
+	}
+	if (host_timing()) {
+		fprintf(stderr, "[dsb host] %lu reads, %lu chunks:", (unsigned long)n, (unsigned long)T.n_chunks);
+		for (int k = 0; k < HS_N; k++)
+			fprintf(stderr, " %s %.1f", hs_name[k], hs[k]);
+		fprintf(stderr, " ms\n");
 	}
 	*max_read_l = carry;
 	if (tl_bytes && getenv("DSB_TIMELINE")) {
