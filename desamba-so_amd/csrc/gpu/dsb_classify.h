@@ -463,68 +463,6 @@ DSB_HD int dsb_isl_step(dsb_isl_t *s, uint32_t mb, uint32_t *so, uint32_t *sl)
 	return 1;
 }
 
-/* Exist bits the scan has already probed, in a 64-position window of the strand (k_island_g,
- * DSB_ISL_MEMO): a grid batch probes positions past the first hit, and a run batch past the end
- * of the run; the batches after them (the hit's run, the grid after the seed) meet some of those
- * positions again, and take their bits from here instead of probing the tables again (tools/
- * island_sim.py: 0.64 -> 0.54 probes per position at grid 8 / run 16 on the C2 proxy).  Same bits,
- * so the same seeds (tests/emu/isl_check.cpp checks every memo bit against the true bit). */
-typedef struct {
-	int32_t kb;            /* window: positions [kb, kb + 64) */
-	uint64_t known, val;   /* bit q - kb: probed / its exist bit */
-} dsb_isl_memo_t;
-
-DSB_HD void dsb_isl_memo_init(dsb_isl_memo_t *m)
-{
-	m->kb = 0;
-	m->known = m->val = 0;
-}
-
-/* move the window so that it holds positions [lo, hi] (hi - lo < 64): forward scans only move up,
- * reverse scans down, so the bits dropped are behind the scan */
-DSB_HD void dsb_isl_memo_cover(dsb_isl_memo_t *m, int fwd, int lo, int hi)
-{
-	if (lo > hi || (lo >= m->kb && hi < m->kb + 64))
-		return;
-	int nkb = fwd ? lo : hi - 63;
-	int sh = nkb - m->kb;
-	if (sh >= 64 || sh <= -64) {
-		m->known = m->val = 0;
-	} else if (sh > 0) {
-		m->known >>= sh;
-		m->val >>= sh;
-	} else if (sh < 0) {
-		m->known <<= -sh;
-		m->val <<= -sh;
-	}
-	m->kb = nkb;
-}
-
-/* the exist bit of position q when the window holds it */
-DSB_HD int dsb_isl_memo_get(const dsb_isl_memo_t *m, int q, int *b)
-{
-	uint32_t o = (uint32_t)(q - m->kb);
-	if (q < 0 || o >= 64 || !((m->known >> o) & 1))
-		return 0;
-	*b = (int)((m->val >> o) & 1);
-	return 1;
-}
-
-/* record a batch's bits (state s before dsb_isl_step; bit g of mb = position dsb_isl_pos(s, g)) */
-template <int GG, int GR>
-DSB_HD void dsb_isl_memo_put(dsb_isl_memo_t *m, const dsb_isl_t *s, uint32_t mb)
-{
-	int G = GG > GR ? GG : GR;
-	for (int g = 0; g < G; g++) {
-		int q = dsb_isl_pos<GG, GR>(s, g);
-		uint32_t o = (uint32_t)(q - m->kb);
-		if (q >= 0 && o < 64) {
-			m->known |= 1ull << o;
-			m->val = (m->val & ~(1ull << o)) | ((uint64_t)((mb >> g) & 1) << o);
-		}
-	}
-}
-
 /* get_seed_vector_M2's top-seed pass (src/cly.c:1190-1225) over seeds as they are produced: after
  * seed m is stored with top = 0, the reference writes one more top byte per seed (0 to the
  * current maximum of the group, or 1 to the maximum of the group seed m closes), and one at the
@@ -3766,6 +3704,9 @@ template <bool WAVE>
 DSB_HDN void dsb_get_score(dsb_read_ws *w, uint32_t l_read)
 {
 	uint64_t tb0 = DSB_T0();
+#ifdef DSB_EXP_BUILD2 /* timing experiment only: the build's marginal cost (the second build rewrites the same tables) */
+	dsb_build_hash_table<WAVE>(w, (int)l_read);
+#endif
 	int key_len = dsb_build_hash_table<WAVE>(w, (int)l_read);
 	DSB_T1(DSB_ST_T_BUILD, tb0);
 	for (uint32_t i = 0; i < w->n_hit; i++) {

@@ -22,7 +22,7 @@
 #define DSB_MINW_DELA 8
 #endif
 #ifndef DSB_MINW_ISLAND
-#define DSB_MINW_ISLAND 8
+#define DSB_MINW_ISLAND 6 /* measured (C2, 300k reads): 8 / 6 waves per SIMD -> island 83.0 / 79.3 ms (15 / 2 VGPRs spilled) */
 #endif
 #ifndef DSB_MINW_RESOLVE
 #define DSB_MINW_RESOLVE 4
@@ -188,9 +188,7 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 #ifndef DSB_ISL_GR
 #define DSB_ISL_GR 0 /* positions per run batch (0: DSB_ISLAND_G) */
 #endif
-#ifndef DSB_ISL_MEMO
-#define DSB_ISL_MEMO 0 /* reuse the bits of positions an earlier batch probed (dsb_isl_memo_t) */
-#endif
+
 template <int G, int STATS>
 __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 								   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
@@ -240,8 +238,6 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 			break;
 		dsb_isl_t s;
 		dsb_isl_init(&s, nk, strand == 0, mine);
-		dsb_isl_memo_t memo;
-		dsb_isl_memo_init(&memo);
 		if (mine)
 			dsb_top_init(&top);
 		for (;;) {
@@ -256,8 +252,6 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 			 * when the batch leaves it; each k-mer's four words come by lane shuffles */
 			int lo, hi;
 			dsb_isl_span<GG, GR>(&s, &lo, &hi);
-			if (DSB_ISL_MEMO && s.mode != DSB_ISL_DONE)
-				dsb_isl_memo_cover(&memo, s.fwd, lo, hi);
 			int64_t klo = ((int64_t)lo + bo) >> 3, khi = (((int64_t)hi + bo) >> 3) + 3;
 			if (s.mode != DSB_ISL_DONE && lo <= hi && (klo < wb || khi >= wb + G)) {
 				wb = s.fwd ? klo : DSB_MAX(khi - (G - 1), wmin);
@@ -282,9 +276,7 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 				uint64_t km = dsb_kmer_at(bin + q, l_ek, sbm);
 #endif
 				pv = (uint32_t)(km & DSB_PRE_IDX_MASK);
-				if (DSB_ISL_MEMO && dsb_isl_memo_get(&memo, q, &b)) {
-					/* probed by an earlier batch */
-				} else if (km) {
+				if (km) {
 					uint64_t h1 = dsb_hash64_1(km) & ix->ek_mask;
 					p1++;
 					if ((dsb_gld(ix->ek0 + (h1 >> 3)) >> (7 - (h1 & 0x7))) & 0x1) {
@@ -297,8 +289,6 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 			uint32_t mb = (uint32_t)(__ballot(b) >> (sg * G)) & GM;
 			if (q >= 0 && (s.mode != DSB_ISL_GRID || (mb && (int)gl == __builtin_ctz(mb))))
 				pre[q] = pv;
-			if (DSB_ISL_MEMO)
-				dsb_isl_memo_put<GG, GR>(&memo, &s, mb);
 			uint32_t so = 0, sl = 0;
 			if (dsb_isl_step<GG, GR>(&s, mb, &so, &sl) && gl == 0) {
 				uint32_t m = top.n, ti;

@@ -1084,6 +1084,11 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			for (uint32_t i = 0; i < cn; i++)
 				if (h_ro[cb + i].status) sel.push_back(i);
 			T.n_retry += sel.size();
+			if (host_timing())
+				for (uint32_t i : sel)
+					fprintf(stderr, "[dsb retry] read %lu L %u scale %u status %#x anchors %u hits %u\n",
+						(unsigned long)(cb + i), len[cb + i], scale[cb + i], h_ro[cb + i].status,
+						h_ro[cb + i].n_anchor, h_ro[cb + i].n_hit);
 			uint64_t tot2 = 0;
 			for (uint32_t i : sel) {
 				scale[cb + i] *= DSB_CAP_RETRY;

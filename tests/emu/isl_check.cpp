@@ -42,39 +42,21 @@ static uint32_t ref_scan(const uint64_t *ex, uint32_t nk, dsb_seed_t *seed_v, ui
 /* the batched form, lanes emulated: the stores k_island_g's group lane 0 makes */
 template <int GG, int GR>
 static uint32_t batch_scan(const uint64_t *ex, uint32_t nk, dsb_seed_t *seed_v, uint32_t dir, uint32_t *total,
-			   uint64_t *probes, int memo, long *memo_bad)
+			   uint64_t *probes)
 {
 	dsb_isl_t s;
 	dsb_isl_init(&s, (int)nk, dir == DSB_FORWARD, 1);
 	dsb_topst_t top;
 	dsb_top_init(&top);
-	dsb_isl_memo_t mm;
-	dsb_isl_memo_init(&mm);
 	while (s.mode != DSB_ISL_DONE) {
 		uint32_t mb = 0;
-		if (memo) { /* k_island_g with DSB_ISL_MEMO: the batch's span in the window first */
-			int lo, hi;
-			dsb_isl_span<GG, GR>(&s, &lo, &hi);
-			dsb_isl_memo_cover(&mm, s.fwd, lo, hi);
-		}
 		for (int g = 0; g < 32; g++) {
 			int q = dsb_isl_pos<GG, GR>(&s, g);
 			if (q >= 0) {
-				int truth = (int)((ex[q >> 6] >> (q & 63)) & 1), b = 0;
-				if (memo && dsb_isl_memo_get(&mm, q, &b)) {
-					if (b != truth) {
-						fprintf(stderr, "memo bit of position %d is %d, the exist bit %d\n", q, b, truth);
-						*memo_bad += 1;
-					}
-				} else {
-					(*probes)++;
-					b = truth;
-				}
-				if (b) mb |= 1u << g;
+				(*probes)++;
+				if ((ex[q >> 6] >> (q & 63)) & 1) mb |= 1u << g;
 			}
 		}
-		if (memo)
-			dsb_isl_memo_put<GG, GR>(&mm, &s, mb);
 		uint32_t so = 0, sl = 0;
 		if (dsb_isl_step<GG, GR>(&s, mb, &so, &sl)) {
 			uint32_t m = top.n, ti;
@@ -91,7 +73,7 @@ static uint32_t batch_scan(const uint64_t *ex, uint32_t nk, dsb_seed_t *seed_v, 
 }
 
 template <int GG, int GR>
-static long check(long trials, uint64_t *probes, uint64_t *positions, uint64_t *memo_probes)
+static long check(long trials, uint64_t *probes, uint64_t *positions)
 {
 	long bad = 0;
 	for (long t = 0; t < trials; t++) {
@@ -113,18 +95,14 @@ static long check(long trials, uint64_t *probes, uint64_t *positions, uint64_t *
 				memcpy(&a[k], &g1, 8);
 				memcpy((char *)&a[k] + 8, &g2, sizeof(dsb_seed_t) - 8);
 			}
-			std::vector<dsb_seed_t> c = a;
 			b = a;
-			uint32_t ta = 0, tb = 0, tc = 0;
+			uint32_t ta = 0, tb = 0;
 			uint32_t la = ref_scan(ex.data(), nk, a.data(), dir, &ta);
-			uint32_t lb = batch_scan<GG, GR>(ex.data(), nk, b.data(), dir, &tb, probes, 0, &bad);
-			uint32_t lc = batch_scan<GG, GR>(ex.data(), nk, c.data(), dir, &tc, memo_probes, 1, &bad);
+			uint32_t lb = batch_scan<GG, GR>(ex.data(), nk, b.data(), dir, &tb, probes);
 			*positions += nk;
-			if (la != lb || ta != tb || memcmp(a.data(), b.data(), cap * sizeof(dsb_seed_t)) || la != lc || ta != tc ||
-			    memcmp(a.data(), c.data(), cap * sizeof(dsb_seed_t))) {
+			if (la != lb || ta != tb || memcmp(a.data(), b.data(), cap * sizeof(dsb_seed_t))) {
 				if (bad < 5)
-					fprintf(stderr, "GG=%d GR=%d nk=%u dir=%u: seeds %u vs %u / %u (memo), total %u vs %u / %u\n", GG, GR, nk,
-						dir, la, lb, lc, ta, tb, tc);
+					fprintf(stderr, "GG=%d GR=%d nk=%u dir=%u: seeds %u vs %u, total %u vs %u\n", GG, GR, nk, dir, la, lb, ta, tb);
 				bad++;
 			}
 		}
@@ -136,18 +114,16 @@ int main(int argc, char **argv)
 {
 	st = argc > 1 ? strtoull(argv[1], 0, 10) | 1 : 1;
 	long n = argc > 2 ? atol(argv[2]) : 20000, bad = 0;
-	uint64_t pr[7] = {0}, pos[7] = {0}, mp[7] = {0};
-	bad += check<4, 4>(n, &pr[0], &pos[0], &mp[0]);
-	bad += check<8, 8>(n, &pr[1], &pos[1], &mp[1]);
-	bad += check<16, 16>(n, &pr[2], &pos[2], &mp[2]);
-	bad += check<32, 32>(n, &pr[3], &pos[3], &mp[3]);
-	bad += check<16, 8>(n, &pr[4], &pos[4], &mp[4]);
-	bad += check<8, 16>(n, &pr[5], &pos[5], &mp[5]);
-	bad += check<12, 16>(n, &pr[6], &pos[6], &mp[6]);
+	uint64_t pr[7] = {0}, pos[7] = {0};
+	bad += check<4, 4>(n, &pr[0], &pos[0]);
+	bad += check<8, 8>(n, &pr[1], &pos[1]);
+	bad += check<16, 16>(n, &pr[2], &pos[2]);
+	bad += check<32, 32>(n, &pr[3], &pos[3]);
+	bad += check<16, 8>(n, &pr[4], &pos[4]);
+	bad += check<8, 16>(n, &pr[5], &pos[5]);
+	bad += check<12, 16>(n, &pr[6], &pos[6]);
 	printf("grid/run 4/4 8/8 16/16 32/32 16/8 8/16 12/16 probes per position:");
 	for (int k = 0; k < 7; k++) printf(" %.3f", (double)pr[k] / pos[k]);
-	printf("\n  with the probed-bit memo (DSB_ISL_MEMO):                       ");
-	for (int k = 0; k < 7; k++) printf(" %.3f", (double)mp[k] / pos[k]);
-	printf("\nisl_check: %ld trials x 2 directions x 7 batch shapes (+ memo), %ld mismatches\n", n, bad);
+	printf("\nisl_check: %ld trials x 2 directions x 7 batch shapes, %ld mismatches\n", n, bad);
 	return bad != 0;
 }
