@@ -64,7 +64,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # the phase kernels of classify part A (kernels.hip launch_phase)
 KERNEL_OF = {"island": "k_island_g<16>", "fast0": "k_wave_phase<1>", "fast1": "k_wave_phase<2>",
              "resolve_f": "k_wave_phase<3>", "slow0": "k_wave_phase<4>", "resolve_s0": "k_wave_phase<5>",
-             "slow1": "k_wave_phase<6>", "resolve_s1": "k_wave_phase<7>", "delA": "k_wave_phase<8>"}
+             "slow1": "k_wave_phase<6>", "resolve_s1": "k_wave_phase<7>", "delA": "k_wave_phase<8>",
+             "hash": "k_hash_lds<0>"}
 
 
 def phase_bytes(c):
@@ -510,14 +511,25 @@ def main():
                 if k.startswith("t_") and k not in ("t_dpm", "t_dps", "t_fill") or (ph == "delA" and k.startswith("t_")):
                     c[k] = tt["stats_phase"][ph][k]
         per_phase = {}
+        hash_lds = phase_ms.get("hash", 0) > 0  # the read hash built in LDS by k_hash_lds before the scoring
         for ph, c in ts["stats_phase"].items():
             b = phase_bytes(c) + (batch.n_bases if ph in ("fast0", "slow0") else 0)
+            if ph == "delA" and hash_lds:  # its hash_b counter is k_hash_lds's work
+                b -= c["hash_b"]
             # the scoring kernel runs twice per chunk when part A is split (slow reads / the rest)
             nl = (tms[0].get("n_launch_dela") or launches) if ph == "delA" else (tms[0].get("n_launch_phase") or launches)
             ms = phase_ms[ph] / nl
             per_phase[ph] = {"algorithmic_bytes_per_launch": int(b / nl), "avg_launch_ms": round(ms, 3),
                              "launches_per_step": nl,
                              "achieved_GBs": round(b / nl / (ms / 1e3) / 1e9, 3) if ms > 0 else None}
+        if hash_lds:
+            nl = tms[0].get("n_launch_dela") or launches
+            hb = ts["stats_phase"]["delA"]["hash_b"]
+            ms = phase_ms["hash"] / nl
+            per_phase["hash"] = {"algorithmic_bytes_per_launch": int(hb / nl), "avg_launch_ms": round(ms, 3),
+                                 "launches_per_step": nl, "achieved_GBs": round(hb / nl / (ms / 1e3) / 1e9, 3) if ms > 0 else None,
+                                 "note": "k_hash_lds: the scoring's read 9-mer hash, head table at the reference's key length "
+                                         "+ 12 B per position (node write, head read / write)"}
         # the Bloom probes (1 B per first / second probe, what one 1-byte gather costs
         # is a 64-B sector) ride in the island block: made by k_island_g itself (the default), or
         # by k_seed over every position before a two-lane island scan of its exist bits

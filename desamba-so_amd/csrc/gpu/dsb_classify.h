@@ -2579,12 +2579,59 @@ DSB_HD int dsb_hash_kl(uint32_t q_len)
 	return key_len < 10 ? 10 : (key_len > 18 ? 18 : key_len);
 }
 
+/* The read hash built in LDS by its own kernel before the scoring (k_hash_lds, DSB_HASH_LDS):
+ * a 2^14-entry head table (64 KB of LDS) holds the key of every read up to 2^23 positions; the
+ * key length is not observable (above), so reads whose dsb_hash_kl is longer use 14 bits. */
+#ifndef DSB_HASH_LDS
+#define DSB_HASH_LDS 0
+#endif
+#define DSB_HASH_LDS_KL 14
+DSB_HD int dsb_hash_lds_read(uint32_t q_len) { return DSB_HASH_LDS && q_len < (1u << 23); }
+DSB_HD int dsb_hash_kl_lds(uint32_t q_len)
+{
+	int kl = dsb_hash_kl(q_len);
+	return kl < DSB_HASH_LDS_KL ? kl : DSB_HASH_LDS_KL;
+}
+/* the reference's key length (src/cly.c:2179-2182): the roofline counts head-table bytes at it */
+DSB_HD int dsb_hash_kl_ref(uint32_t q_len)
+{
+	int key_len = 10;
+	for (; key_len < 18; key_len++)
+		if ((int64_t)(1u << key_len) >= (int64_t)q_len)
+			break;
+	return key_len;
+}
+
+/* the strands the scoring looks up (get_score_M2 via delete_small_score_rst, src/cly.c:2186-2194):
+ * bit 1 forward, bit 0 reverse, over the hits the scoring keeps (dsb_delete_small_A's trim) */
+DSB_HD int dsb_hash_dirs(const dsb_read_ws *w)
+{
+	uint32_t n = w->n_hit;
+	if (n > 200) {
+		uint32_t rst_num = 200;
+		for (; rst_num < n && w->hit[rst_num].sum_score > 50; rst_num++);
+		n = rst_num;
+	}
+	n = DSB_MIN(400u, n);
+	int both_dir = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		both_dir |= (w->hit[i].direction == DSB_FORWARD) ? 0x2 : 0x1;
+		if (both_dir == 3)
+			break;
+	}
+	return both_dir;
+}
+
 /* build_hash_table_M2, src/cly.c:2168-2219: chained 9-mer hash of the read, per strand.
  * Lists hold positions in increasing order (the reference appends in position order), built
  * here from the last position backwards so that only the heads array is needed. */
 template <bool WAVE>
 DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 {
+#if defined(__HIP_DEVICE_COMPILE__)
+	if (WAVE && dsb_hash_lds_read((uint32_t)q_len))
+		return dsb_hash_kl_lds((uint32_t)q_len); /* built by k_hash_lds before this launch */
+#endif
 	int both_dir = 0;
 	for (uint32_t i = 0; i < w->n_hit; i++) {
 		both_dir |= (w->hit[i].direction == DSB_FORWARD) ? 0x2 : 0x1;
@@ -2616,7 +2663,9 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 			 * higher lane with its key (its list successor) and whether a lower lane has it */
 			uint32_t lane = dsb_lane();
 			for (uint32_t k = lane; k <= KEY_MASK; k += DSB_WV) heads[k] = DSB_HEMPTY;
-			if (w->stats && lane == 0) w->stats[DSB_ST_HASH_B] += 4ull * (KEY_MASK + 1);
+			/* algorithmic bytes: the head table at the reference's key length (a longer key is an
+			 * implementation choice, not work), + 12 B per position below */
+			if (w->stats && lane == 0) w->stats[DSB_ST_HASH_B] += 4ull << dsb_hash_kl_ref((uint32_t)q_len);
 			dsb_wsync();
 			for (int cb = n_pos > 0 ? ((n_pos - 1) & ~(DSB_WV - 1)) : -1; cb >= 0; cb -= DSB_WV) {
 				int c_pos = cb + (int)lane;

@@ -175,6 +175,15 @@ __global__ __launch_bounds__(256) void k_taxon_count(const uint32_t *__restrict_
 		atomicAdd(counts + tid[i], weight ? (unsigned long long)weight[i] : 1ull);
 }
 
+/* dst[idx[i]] = src[i] (the per-read taxa of the deferred re-runs into the batch's table) */
+__global__ __launch_bounds__(256) void k_scatter_u32(uint32_t *__restrict__ dst, const uint32_t *__restrict__ idx,
+						     const uint32_t *__restrict__ src, uint32_t n)
+{
+	uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n)
+		dst[idx[i]] = src[i];
+}
+
 /* The merge-sort orders the classifier depends on, one array per lane:
  * which 0 chain_cmp_by_pos, 1 chain_cmp_by_MEM_score, 2 chain_cmp_by_score, 3 anchors
  * (Anchor_cmp_by_chr_ID_and_pos), 4 MEM_rst by match_len.  Output: permutation in idx. */
@@ -260,6 +269,9 @@ struct dsb_gpu_dev {
 	dsb_dindex_t *d;         /* device copy */
 	std::vector<void *> allocs;
 	dbuf ws_off, scale, ws, wsr, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2, woA, woB;
+	dbuf vlen, vso, vidx, vtid; /* the deferred overflow re-runs of a batch (batch_run) */
+	hipEvent_t evh[2][2];    /* k_hash_lds before the scoring launch, per stream (launch_phase) */
+	int evh_used[2] = {0, 0};
 	uint32_t tag = 0;        /* tag of this context's last phase launch (dsb_hset_tag; next_launch_tag) */
 	/* streamed batches (read_classify pipeline): uploads on their own stream through pinned
 	 * staging, under their own lock, beside the kernels of the batch before */
@@ -320,6 +332,9 @@ static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu
 	HIP_OK(hipEventCreate(&g->ev_fork));
 	HIP_OK(hipEventCreate(&g->ev_r0));
 	HIP_OK(hipEventCreate(&g->ev_r1));
+	for (int k = 0; k < 2; k++)
+		for (int e = 0; e < 2; e++)
+			HIP_OK(hipEventCreate(&g->evh[k][e]));
 	for (int k = 0; k < 2; k++)
 		for (int ph = 0; ph <= DSB_PH_N; ph++)
 			for (int e = 0; e < 2; e++)
@@ -607,6 +622,24 @@ static uint32_t wave_phases(void)
 static std::atomic<uint32_t> g_launch_tag{0};
 static uint32_t next_launch_tag(void) { return ++g_launch_tag; }
 
+/* the LDS read-hash build's time (ms_phase[DSB_PH_HASH]) since the last call, taken out of the
+ * scoring phase's (the callers time the hash build + scoring launch pair together); the events
+ * of launches the callers do not time (overflow re-runs) are dropped with clear = 1 */
+#define DSB_PH_HASH 9
+static float hash_ms(dsb_gpu_dev *g, int clear = 0)
+{
+	float tot = 0;
+	for (int si = 0; si < 2; si++)
+		if (g->evh_used[si]) {
+			float ms = 0;
+			if (!clear && hipEventSynchronize(g->evh[si][1]) == hipSuccess &&
+			    hipEventElapsedTime(&ms, g->evh[si][0], g->evh[si][1]) == hipSuccess)
+				tot += ms;
+			g->evh_used[si] = 0;
+		}
+	return tot;
+}
+
 /* one phase of part A over the reads order[0..m) */
 static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, uint8_t *wsb, const uint32_t *order,
 			 uint32_t m, hipStream_t s = 0)
@@ -632,6 +665,19 @@ static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, 
 		hipStreamSynchronize(s);
 	}
 	uint32_t tag = g->tag;
+	if (ph == DSB_PH_DELA && DSB_HASH_LDS && m) {
+		/* the read hash in LDS (k_hash_lds), then the scoring; timed apart by hash_ms() */
+		int si = s == g->stream2;
+		hipEventRecord(g->evh[si][0], s);
+		if (stats == 1)
+			hipLaunchKernelGGL(k_hash_lds<1>, dim3(2 * m), dim3(DSB_HL_WG), 0, s, g->d, cl, g->ws_off.as<uint64_t>(),
+					   g->scale.as<uint32_t>(), wsb, order, m, g->stats.as<unsigned long long>());
+		else
+			hipLaunchKernelGGL(k_hash_lds<0>, dim3(2 * m), dim3(DSB_HL_WG), 0, s, g->d, cl, g->ws_off.as<uint64_t>(),
+					   g->scale.as<uint32_t>(), wsb, order, m, g->stats.as<unsigned long long>());
+		hipEventRecord(g->evh[si][1], s);
+		g->evh_used[si] = 1;
+	}
 	if (wave)
 		hipLaunchKernelGGL(fn, dim3(m), dim3(64), 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
@@ -835,6 +881,11 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 	hipEventElapsedTime(&wall, g->ev_fork, g->ev_b);
 	hipEventElapsedTime(&rest, g->ev_r0, g->ev_r1);
 	T.ms_phase[DSB_PH_DELA] += rest; /* both scoring launches; ms_classA takes the overlapped wall time */
+	{
+		float hm = hash_ms(g); /* both launches' read-hash builds (each timed with its scoring launch) */
+		T.ms_phase[DSB_PH_HASH] += hm;
+		T.ms_phase[DSB_PH_DELA] -= hm;
+	}
 	T.ms_classA += wall;
 	T.n_launch_dela += 2;
 	return 1;
@@ -850,6 +901,39 @@ static int host_timing(void)
 	if (v < 0)
 		v = getenv("DSB_HOST_TIMING") ? 1 : 0;
 	return v;
+}
+
+/* overflow re-runs deferred to the end of a batch when they cannot change the carry (batch_run);
+ * DSB_DEFER_RETRY=0 re-runs them chunk by chunk */
+static int defer_retries(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("DSB_DEFER_RETRY");
+		v = e ? (atoi(e) != 0) : 1;
+	}
+	return v;
+}
+
+/* part B (k_classB) of the reads order[0, n) of a view: lengths cl, the context's ws_off / scale /
+ * mrl / ro / hit_off arrays, per-read taxa to tid */
+static int launch_classB(dsb_gpu_dev *g, dsb_gpu_batch *b, const uint32_t *cl, uint8_t *wsb, const uint32_t *order,
+			 uint32_t n, uint32_t *tid, int stats_on, hipStream_t s)
+{
+	(void)b;
+	if (n == 0)
+		return 0;
+	if (stats_on == 1)
+		k_classB<true><<<(n + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, n,
+							 g->mrl.as<int32_t>(), g->ro.as<dsb_read_out_t>(), g->hits.as<dsb_hit_out_t>(),
+							 g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(), tid,
+							 g->stats.as<unsigned long long>());
+	else
+		k_classB<false><<<(n + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, n,
+							  g->mrl.as<int32_t>(), g->ro.as<dsb_read_out_t>(), g->hits.as<dsb_hit_out_t>(),
+							  g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(), tid,
+							  g->stats.as<unsigned long long>());
+	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on,
@@ -908,9 +992,92 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	std::vector<uint64_t> word_off;
 	dsb_read_out_t *ro = b->ro.data();
 	std::vector<dsb_hit_out_t> &hv = b->hits;
+	std::vector<uint64_t> deferred; /* overflowed reads whose re-run waits for the end of the batch */
 	size_t budget = ws_budget(g, hooks ? g->n_ctx : 1);
 	int carry = *max_read_l;
 	int l_ek = ix->l_ek;
+	/* ---- overflow: re-run the reads i < cn of a view whose flag is set, with 8x capacities in the
+	 * retry buffer; the view's host arrays are indexed cb + i, its device lengths / sequence offsets
+	 * are cl[i] / cso[i]: one chunk, or the deferred overflows of the whole batch (below) */
+	auto retry_view = [&](uint32_t cn, uint64_t cb, const std::vector<uint32_t> &vlen, std::vector<uint32_t> &vscale,
+			      std::vector<uint64_t> &vws_off, std::vector<dsb_read_out_t> &vro, const uint32_t *cl,
+			      const uint64_t *cso, uint8_t *wsb, uint64_t &rused, uint32_t n_over) -> int {
+		while (n_over) {
+			std::vector<uint32_t> sel;
+			for (uint32_t i = 0; i < cn; i++)
+				if (vro[cb + i].status) sel.push_back(i);
+			T.n_retry += sel.size();
+			if (host_timing())
+				for (uint32_t i : sel)
+					fprintf(stderr, "[dsb retry] read %lu L %u scale %u status %#x anchors %u hits %u\n",
+						(unsigned long)(cb + i), vlen[cb + i], vscale[cb + i], vro[cb + i].status,
+						vro[cb + i].n_anchor, vro[cb + i].n_hit);
+			uint64_t tot2 = 0;
+			for (uint32_t i : sel) {
+				vscale[cb + i] *= DSB_CAP_RETRY;
+				if (vscale[cb + i] > 4096 * DSB_SCALE_UNIT) {
+					snprintf(err, errn, "read %lu overflows every workspace size", (unsigned long)(cb + i));
+					return -1;
+				}
+				vws_off[cb + i] = tot2; /* within this round's part of the retry buffer (rebased below) */
+				tot2 += dsb_layout(vlen[cb + i], dsb_default_caps(vlen[cb + i], vscale[cb + i])).total;
+			}
+			/* the re-run reads live in a separate retry buffer (reads of earlier rounds keep their
+			 * bytes; growing it copies only those), addressed from the chunk's base pointer: a
+			 * read's offset is (retry buffer - chunk buffer) + its place there, modulo 2^64, so
+			 * every kernel keeps using ws + ws_off[r] and the chunk workspace is never duplicated */
+			if (rused + tot2 + 4096 > g->wsr.cap) {
+				void *np = nullptr;
+				size_t need = rused + tot2 + (rused + tot2) / 2 + 4096;
+				HIP_OK(hipMalloc(&np, need));
+				HIP_OK(hipMemsetAsync(np, 0, need, s));
+				if (rused)
+					HIP_OK(hipMemcpyAsync(np, g->wsr.p, rused, hipMemcpyDeviceToDevice, s));
+				HIP_OK(hipStreamSynchronize(s));
+				uint64_t delta = (uint64_t)(uintptr_t)np - (uint64_t)(uintptr_t)g->wsr.p;
+				for (uint32_t i = 0; i < cn; i++) /* earlier retried reads move with the buffer */
+					if (vscale[cb + i] > scale0 && !std::binary_search(sel.begin(), sel.end(), i))
+						vws_off[cb + i] += delta;
+				if (g->wsr.p)
+					hipFree(g->wsr.p);
+				g->wsr.p = np;
+				g->wsr.cap = need;
+			}
+			{
+				uint64_t rbase = (uint64_t)(uintptr_t)g->wsr.p - (uint64_t)(uintptr_t)wsb + rused;
+				for (uint32_t i : sel)
+					vws_off[cb + i] += rbase;
+				rused += tot2;
+			}
+			HIP_OK(hipMemcpyAsync(g->ws_off.p, vws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
+			HIP_OK(hipMemcpyAsync(g->scale.p, vscale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
+			std::vector<uint64_t> wo2;
+			uint64_t tw2 = seed_words(vlen, cb, sel.data(), sel.size(), l_ek, wo2, nullptr);
+			if (g->sel.ensure(4 * sel.size() + 4, err, errn) || g->wo2.ensure(8 * wo2.size() + 16, err, errn))
+				return -1;
+			HIP_OK(hipMemcpyAsync(g->sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(hipMemcpyAsync(g->wo2.p, wo2.data(), 8 * wo2.size(), hipMemcpyHostToDevice, s));
+			uint32_t m = (uint32_t)sel.size();
+			if (m == 0) {
+				snprintf(err, errn, "overflow reported by the phase kernels but no read carries the flag");
+				return -1;
+			}
+			k_encode<<<m, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, g->sel.as<uint32_t>(), m);
+			if (tw2 && DSB_ISLAND_G == 0)
+				k_seed<<<(uint32_t)((tw2 * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
+											      g->wo2.as<uint64_t>(), g->sel.as<uint32_t>(), m, tw2, nullptr);
+			HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
+			for (int ph = 0; ph < DSB_PH_N; ph++)
+				launch_phase(g, ph, false, cl, wsb, g->sel.as<uint32_t>(), m);
+			HIP_OK(hipGetLastError());
+			/* the re-run went to the non-blocking stream: drain it before the (null-stream) copies */
+			HIP_OK(hipStreamSynchronize(s));
+			hash_ms(g, 1); /* re-runs are not timed */
+			HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
+			HIP_OK(hipMemcpy(vro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
+		}
+		return 0;
+	};
 	hs_mark(HS_SETUP);
 	for (uint64_t cb = 0; cb < n;) {
 		/* ---- chunk [cb, ce) within the workspace budget, input order */
@@ -1060,8 +1227,12 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			float ms = ev_ms(g);
 			T.ms_phase[ph] += ms;
 			T.ms_classA += ms;
-			if (ph == DSB_PH_DELA)
+			if (ph == DSB_PH_DELA) {
 				T.n_launch_dela++;
+				float hm = hash_ms(g);
+				T.ms_phase[DSB_PH_HASH] += hm;
+				T.ms_phase[DSB_PH_DELA] -= hm;
+			}
 			HIP_OK(hipGetLastError());
 			if (ph == DSB_PH_RESOLVE_F && split_slow()) {
 				int r = run_split(g, stats_on, cl, wsb, cn, T, err, errn);
@@ -1078,80 +1249,37 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
 		HIP_OK(hipMemcpy(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
 		hs_mark(HS_SYNC_A);
-		/* ---- overflow: re-run those reads with 8x capacities in extra workspace */
-		while (n_over) {
-			std::vector<uint32_t> sel;
-			for (uint32_t i = 0; i < cn; i++)
-				if (h_ro[cb + i].status) sel.push_back(i);
-			T.n_retry += sel.size();
-			if (host_timing())
-				for (uint32_t i : sel)
-					fprintf(stderr, "[dsb retry] read %lu L %u scale %u status %#x anchors %u hits %u\n",
-						(unsigned long)(cb + i), len[cb + i], scale[cb + i], h_ro[cb + i].status,
-						h_ro[cb + i].n_anchor, h_ro[cb + i].n_hit);
-			uint64_t tot2 = 0;
-			for (uint32_t i : sel) {
-				scale[cb + i] *= DSB_CAP_RETRY;
-				if (scale[cb + i] > 4096 * DSB_SCALE_UNIT) {
-					snprintf(err, errn, "read %lu overflows every workspace size", (unsigned long)(cb + i));
-					return -1;
-				}
-				ws_off[cb + i] = tot2; /* within this round's part of the retry buffer (rebased below) */
-				tot2 += dsb_layout(len[cb + i], dsb_default_caps(len[cb + i], scale[cb + i])).total;
+		/* ---- max_read_l carry (src/cly.c:2953): prefix max over reads reaching the update; a
+		 * streamed batch takes its carry-in from the batch before it (possibly on another GPU)
+		 * once its own part A is done, and hands its carry-out on before its part B */
+		if (cb == 0 && hooks && hooks->carry_in)
+			carry = hooks->carry_in(hooks->ctx);
+		/* ---- overflow: re-run those reads now, or defer them to one re-run at the end of the
+		 * batch.  A deferred read's own part A result (reached_update) must not matter to the
+		 * carry, i.e. the carry before it is already >= its length; then the chunk's part B runs
+		 * for every other read now and the chunk's workspace is free for the next chunk (the
+		 * re-run lives in the retry buffer).  A chunk re-run costs a launch of every phase on a
+		 * few long-running waves (~10 ms on the C2 proxy, about one read per 110k-read chunk). */
+		uint32_t n_def = 0;
+		if (n_over && defer_retries()) {
+			int c = carry, ok = 1;
+			for (uint32_t i = 0; i < cn && ok; i++) {
+				if (h_ro[cb + i].status)
+					ok = (int)len[cb + i] <= c;
+				else if (h_ro[cb + i].reached_update && (int)len[cb + i] > c)
+					c = (int)len[cb + i];
 			}
-			/* the re-run reads live in a separate retry buffer (reads of earlier rounds keep their
-			 * bytes; growing it copies only those), addressed from the chunk's base pointer: a
-			 * read's offset is (retry buffer - chunk buffer) + its place there, modulo 2^64, so
-			 * every kernel keeps using ws + ws_off[r] and the chunk workspace is never duplicated */
-			if (rused + tot2 + 4096 > g->wsr.cap) {
-				void *np = nullptr;
-				size_t need = rused + tot2 + (rused + tot2) / 2 + 4096;
-				HIP_OK(hipMalloc(&np, need));
-				HIP_OK(hipMemsetAsync(np, 0, need, s));
-				if (rused)
-					HIP_OK(hipMemcpyAsync(np, g->wsr.p, rused, hipMemcpyDeviceToDevice, s));
-				HIP_OK(hipStreamSynchronize(s));
-				uint64_t delta = (uint64_t)(uintptr_t)np - (uint64_t)(uintptr_t)g->wsr.p;
-				for (uint32_t i = 0; i < cn; i++) /* earlier retried reads move with the buffer */
-					if (scale[cb + i] > scale0 && !std::binary_search(sel.begin(), sel.end(), i))
-						ws_off[cb + i] += delta;
-				if (g->wsr.p)
-					hipFree(g->wsr.p);
-				g->wsr.p = np;
-				g->wsr.cap = need;
+			if (ok) {
+				for (uint32_t i = 0; i < cn; i++)
+					if (h_ro[cb + i].status) {
+						deferred.push_back(cb + i);
+						n_def++;
+					}
+				n_over = 0;
 			}
-			{
-				uint64_t rbase = (uint64_t)(uintptr_t)g->wsr.p - (uint64_t)(uintptr_t)wsb + rused;
-				for (uint32_t i : sel)
-					ws_off[cb + i] += rbase;
-				rused += tot2;
-			}
-			HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
-			HIP_OK(hipMemcpyAsync(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
-			std::vector<uint64_t> wo2;
-			uint64_t tw2 = seed_words(len, cb, sel.data(), sel.size(), l_ek, wo2, nullptr);
-			if (g->sel.ensure(4 * sel.size() + 4, err, errn) || g->wo2.ensure(8 * wo2.size() + 16, err, errn))
-				return -1;
-			HIP_OK(hipMemcpyAsync(g->sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, s));
-			HIP_OK(hipMemcpyAsync(g->wo2.p, wo2.data(), 8 * wo2.size(), hipMemcpyHostToDevice, s));
-			uint32_t m = (uint32_t)sel.size();
-			if (m == 0) {
-				snprintf(err, errn, "overflow reported by the phase kernels but no read carries the flag");
-				return -1;
-			}
-			k_encode<<<m, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, g->sel.as<uint32_t>(), m);
-			if (tw2 && DSB_ISLAND_G == 0)
-				k_seed<<<(uint32_t)((tw2 * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
-											      g->wo2.as<uint64_t>(), g->sel.as<uint32_t>(), m, tw2, nullptr);
-			HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
-			for (int ph = 0; ph < DSB_PH_N; ph++)
-				launch_phase(g, ph, false, cl, wsb, g->sel.as<uint32_t>(), m);
-			HIP_OK(hipGetLastError());
-			/* the re-run went to the non-blocking stream: drain it before the (null-stream) copies */
-			HIP_OK(hipStreamSynchronize(s));
-			HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
-			HIP_OK(hipMemcpy(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
 		}
+		if (n_over && retry_view(cn, cb, len, scale, ws_off, h_ro, cl, cso, wsb, rused, n_over))
+			return -1;
 		hs_mark(HS_RETRY);
 		if (getenv("DSB_DEBUG_READ")) { /* diagnostic: dump one read's workspace after stage A */
 			uint64_t dr = strtoull(getenv("DSB_DEBUG_READ"), NULL, 10);
@@ -1171,11 +1299,6 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				dsb_debug_dump(stderr, &w, "gpuA");
 			}
 		}
-		/* ---- max_read_l carry (src/cly.c:2953): prefix max over reads reaching the update; a
-		 * streamed batch takes its carry-in from the batch before it (possibly on another GPU)
-		 * once its own part A is done, and hands its carry-out on before its part B */
-		if (cb == 0 && hooks && hooks->carry_in)
-			carry = hooks->carry_in(hooks->ctx);
 		uint64_t worst = 0;
 		for (uint32_t i = 0; i < cn; i++) {
 			if (h_ro[cb + i].reached_update && (int)len[cb + i] > carry)
@@ -1189,17 +1312,19 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		if (g->hits.ensure(sizeof(dsb_hit_out_t) * worst + 4096, err, errn))
 			return -1;
 		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
+		uint32_t cnB = cn;
+		if (n_def) { /* part B of this chunk: every read but the deferred ones */
+			std::vector<uint32_t> ordB;
+			ordB.reserve(cn - n_def);
+			for (uint32_t i : order)
+				if (!h_ro[cb + i].status)
+					ordB.push_back(i);
+			cnB = (uint32_t)ordB.size();
+			HIP_OK(hipMemcpy(g->order.p, ordB.data(), 4ull * cnB, hipMemcpyHostToDevice));
+		}
 		hipEventRecord(g->ev_a, s);
-		if (stats_on == 1)
-			k_classB<true><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
-							 g->order.as<uint32_t>(), cn, g->mrl.as<int32_t>(), g->ro.as<dsb_read_out_t>(),
-							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(),
-							 b->d_tid.as<uint32_t>() + cb, g->stats.as<unsigned long long>());
-		else
-			k_classB<false><<<(cn + 63) / 64, 64, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
-							 g->order.as<uint32_t>(), cn, g->mrl.as<int32_t>(), g->ro.as<dsb_read_out_t>(),
-							 g->hits.as<dsb_hit_out_t>(), g->cnt.as<uint32_t>(), g->hit_off.as<uint32_t>(),
-							 b->d_tid.as<uint32_t>() + cb, g->stats.as<unsigned long long>());
+		if (launch_classB(g, b, cl, wsb, g->order.as<uint32_t>(), cnB, b->d_tid.as<uint32_t>() + cb, stats_on, s))
+			return -1;
 		T.ms_classB += ev_ms(g);
 		HIP_OK(hipGetLastError());
 		hs_mark(HS_CARRY_B);
@@ -1223,6 +1348,66 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		for (int k = 0; k < HS_N; k++)
 			fprintf(stderr, " %s %.1f", hs_name[k], hs[k]);
 		fprintf(stderr, " ms\n");
+	}
+	/* ---- the deferred overflow re-runs of every chunk together, then their part B */
+	if (!deferred.empty()) {
+		uint32_t m = (uint32_t)deferred.size();
+		std::vector<uint32_t> vlen(m), vscale(m), vidx(m);
+		std::vector<uint64_t> vws(m, 0), vso(m);
+		std::vector<dsb_read_out_t> vro(m);
+		std::vector<int32_t> vmrl(m);
+		for (uint32_t k = 0; k < m; k++) {
+			uint64_t r = deferred[k];
+			vidx[k] = (uint32_t)r;
+			vlen[k] = len[r];
+			vscale[k] = scale[r];
+			vso[k] = b->seq_off[r];
+			vro[k] = ro[r]; /* part A's result: the overflow flag set */
+			vmrl[k] = mrl[r];
+		}
+		if (g->vlen.ensure(4ull * m + 4, err, errn) || g->vso.ensure(8ull * m + 8, err, errn) ||
+		    g->vidx.ensure(4ull * m + 4, err, errn) || g->vtid.ensure(4ull * m + 4, err, errn))
+			return -1;
+		HIP_OK(hipMemcpy(g->vlen.p, vlen.data(), 4ull * m, hipMemcpyHostToDevice));
+		HIP_OK(hipMemcpy(g->vso.p, vso.data(), 8ull * m, hipMemcpyHostToDevice));
+		HIP_OK(hipMemcpy(g->vidx.p, vidx.data(), 4ull * m, hipMemcpyHostToDevice));
+		uint64_t rused = 0;
+		uint8_t *wsb = g->ws.as<uint8_t>();
+		const uint32_t *vcl = g->vlen.as<uint32_t>();
+		if (retry_view(m, 0, vlen, vscale, vws, vro, vcl, g->vso.as<uint64_t>(), wsb, rused, m))
+			return -1;
+		std::vector<uint32_t> vord(m);
+		uint64_t worst = 0;
+		for (uint32_t k = 0; k < m; k++) {
+			vord[k] = k;
+			worst += vro[k].n_hit;
+		}
+		HIP_OK(hipMemcpy(g->order.p, vord.data(), 4ull * m, hipMemcpyHostToDevice));
+		HIP_OK(hipMemcpy(g->mrl.p, vmrl.data(), 4ull * m, hipMemcpyHostToDevice));
+		if (g->hits.ensure(sizeof(dsb_hit_out_t) * worst + 4096, err, errn))
+			return -1;
+		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
+		hipEventRecord(g->ev_a, s);
+		if (launch_classB(g, b, vcl, wsb, g->order.as<uint32_t>(), m, g->vtid.as<uint32_t>(), stats_on, s))
+			return -1;
+		k_scatter_u32<<<(m + 255) / 256, 256, 0, s>>>(b->d_tid.as<uint32_t>(), g->vidx.as<uint32_t>(),
+								 g->vtid.as<uint32_t>(), m);
+		T.ms_classB += ev_ms(g);
+		HIP_OK(hipGetLastError());
+		uint32_t nh = 0;
+		std::vector<uint32_t> voff(m);
+		HIP_OK(hipMemcpy(&nh, g->cnt.p, 4, hipMemcpyDeviceToHost));
+		HIP_OK(hipMemcpy(vro.data(), g->ro.p, sizeof(dsb_read_out_t) * m, hipMemcpyDeviceToHost));
+		HIP_OK(hipMemcpy(voff.data(), g->hit_off.p, 4ull * m, hipMemcpyDeviceToHost));
+		uint64_t base = hv.size();
+		hv.resize(base + nh);
+		if (nh)
+			HIP_OK(hipMemcpy(hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost));
+		for (uint32_t k = 0; k < m; k++) {
+			ro[deferred[k]] = vro[k];
+			ro[deferred[k]].hit_off = base + voff[k];
+		}
+		hs_mark(HS_RETRY);
 	}
 	*max_read_l = carry;
 	if (tl_bytes && getenv("DSB_TIMELINE")) {

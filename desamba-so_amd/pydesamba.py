@@ -14,6 +14,9 @@ LIB_PATH = os.path.join(HERE, "lib", "libdesamba.so")
 
 FMT_SAM, FMT_SAM_FULL, FMT_DES, FMT_DES_FULL = 1, 2, 3, 4
 PHASES = ["island", "fast0", "fast1", "resolve_f", "slow0", "resolve_s0", "slow1", "resolve_s1", "delA"]
+# ms_phase slots: the phases (each with a work-counter block), then the scoring's read-hash build in
+# LDS (k_hash_lds, DSB_HASH_LDS builds; its counters are in the delA block, hash_b)
+MS_PHASES = PHASES + ["hash"]
 ST_NAMES = ["occ", "occ_nib", "mem_search", "sa", "uni", "ref_pos", "getref_b", "anchor", "chain", "ek1", "ek2",
             "hash_b", "lookup", "node", "t_mem", "t_map", "t_build", "t_match", "t_win", "t_all", "t_dpm", "t_dps",
             "t_fill", "pass2", "replay", "t_mprobe", "t_mwalk", "t_comb", "nwin", "nbatch", "ncand", "nsms"]
@@ -34,7 +37,7 @@ class Timing(C.Structure):
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("stats", "ms_phase")}
-        d["ms_phase"] = {n: float(self.ms_phase[i]) for i, n in enumerate(PHASES)}
+        d["ms_phase"] = {n: float(self.ms_phase[i]) for i, n in enumerate(MS_PHASES)}
         d["stats_phase"] = {ph: {n: int(self.stats[ST_STRIDE * p + i]) for i, n in enumerate(ST_NAMES)}
                             for p, ph in enumerate(PHASES)}
         d["stats"] = {n: sum(v[n] for v in d["stats_phase"].values()) for n in ST_NAMES}
