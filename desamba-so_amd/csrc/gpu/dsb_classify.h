@@ -2585,7 +2585,9 @@ DSB_HD int dsb_hash_kl(uint32_t q_len)
 #ifndef DSB_HASH_LDS
 #define DSB_HASH_LDS 0
 #endif
+#ifndef DSB_HASH_LDS_KL
 #define DSB_HASH_LDS_KL 14
+#endif
 DSB_HD int dsb_hash_lds_read(uint32_t q_len) { return DSB_HASH_LDS && q_len < (1u << 23); }
 DSB_HD int dsb_hash_kl_lds(uint32_t q_len)
 {

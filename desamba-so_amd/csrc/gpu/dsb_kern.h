@@ -374,7 +374,7 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 #define DSB_HL_WG 256
 #define DSB_HL_SLOTS 4096
 template <int STATS>
-__global__ __launch_bounds__(DSB_HL_WG, 2) void k_hash_lds(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+__global__ __launch_bounds__(DSB_HL_WG, DSB_HASH_LDS_KL <= 13 ? 4 : 2) void k_hash_lds(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 							 const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 							 uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 							 unsigned long long *__restrict__ gstats)
@@ -417,16 +417,19 @@ __global__ __launch_bounds__(DSB_HL_WG, 2) void k_hash_lds(const dsb_dindex_t *_
 		/* head table at the reference's key length + per position: the node write, head read and write */
 		atomicAdd(st + DSB_ST_HASH_B, (unsigned long long)(4ull * (1ull << dsb_hash_kl_ref(L)) + 12ull * n_pos));
 	}
-	/* the block's k-mers, loaded one block ahead */
+	/* the blocks' k-mers, loaded four blocks ahead (a block's LDS work is shorter than a load) */
 	int cb = (n_pos - 1) & ~(DSB_HL_WG - 1);
-	uint32_t kmer = ((int)(cb + tid) < n_pos) ? dsb_q9mer(q + cb + tid) : 0;
+	auto ld = [&](int b) -> uint32_t { return (b >= 0 && b + (int)tid < n_pos) ? dsb_q9mer(q + b + tid) : 0; };
+	uint32_t k0 = ld(cb), k1 = ld(cb - DSB_HL_WG), k2 = ld(cb - 2 * DSB_HL_WG), k3 = ld(cb - 3 * DSB_HL_WG);
 	__syncthreads();
 	for (; cb >= 0; cb -= DSB_HL_WG) {
 		int c_pos = cb + (int)tid;
 		int act = c_pos < n_pos;
-		uint32_t km = kmer;
-		if (cb >= DSB_HL_WG)
-			kmer = dsb_q9mer(q + cb - DSB_HL_WG + tid);
+		uint32_t km = k0;
+		k0 = k1;
+		k1 = k2;
+		k2 = k3;
+		k3 = ld(cb - 4 * DSB_HL_WG);
 		int key = act ? (int)(km & KEY_MASK) : -1 - (int)tid;
 		keyl[tid] = (uint32_t)key;
 		if (tid == 0)
@@ -464,8 +467,11 @@ __global__ __launch_bounds__(DSB_HL_WG, 2) void k_hash_lds(const dsb_dindex_t *_
 			if (!has_prev)
 				heads[key] = ent;
 		}
-		__syncthreads();
+		/* no barrier here: the next block's first LDS writes (keys, slots, the loser count) touch
+		 * nothing this block reads after the barrier above, and its head reads follow its own
+		 * first barrier */
 	}
+	__syncthreads();
 	for (uint32_t k = tid; k <= KEY_MASK; k += DSB_HL_WG) g_heads[k] = heads[k];
 }
 
