@@ -2635,10 +2635,20 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 		return dsb_hash_kl_lds((uint32_t)q_len); /* built by k_hash_lds before this launch */
 #endif
 	int both_dir = 0;
-	for (uint32_t i = 0; i < w->n_hit; i++) {
-		both_dir |= (w->hit[i].direction == DSB_FORWARD) ? 0x2 : 0x1;
-		if (both_dir == 3)
-			break;
+	if (!WAVE || DSB_SEQ(w, 1)) {
+		for (uint32_t i = 0; i < w->n_hit; i++) {
+			both_dir |= (w->hit[i].direction == DSB_FORWARD) ? 0x2 : 0x1;
+			if (both_dir == 3)
+				break;
+		}
+	} else {
+		/* the hits' directions 64 at a time (one round trip per 64 hits, not one per hit) */
+		uint32_t lane = dsb_lane();
+		for (uint32_t gb = 0; gb < w->n_hit && both_dir != 3; gb += DSB_WV) {
+			uint32_t i = gb + lane;
+			int d = i < w->n_hit ? (w->hit[i].direction == DSB_FORWARD ? 2 : 1) : 0;
+			both_dir |= (dsb_wballot(d == 2) ? 2 : 0) | (dsb_wballot(d == 1) ? 1 : 0);
+		}
 	}
 	int key_len = dsb_hash_kl((uint32_t)q_len);
 	uint32_t KEY_MASK = (1u << key_len) - 1;

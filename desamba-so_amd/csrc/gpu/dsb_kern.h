@@ -383,7 +383,7 @@ __global__ __launch_bounds__(DSB_HL_WG, DSB_HASH_LDS_KL <= 13 ? 4 : 2) void k_ha
 	__shared__ uint8_t slot[DSB_HL_SLOTS];
 	__shared__ uint32_t keyl[DSB_HL_WG], entl[DSB_HL_WG];
 	__shared__ uint16_t losers[DSB_HL_WG], wonl[DSB_HL_WG];
-	__shared__ uint32_t n_los;
+	__shared__ uint32_t n_los, sh_n, sh_dirs;
 	uint32_t t = blockIdx.x >> 1, h = blockIdx.x & 1, tid = threadIdx.x;
 	if (t >= n)
 		return;
@@ -400,7 +400,23 @@ __global__ __launch_bounds__(DSB_HL_WG, DSB_HASH_LDS_KL <= 13 ? 4 : 2) void k_ha
 	dsb_state_load(&w, &f, (const dsb_rstate_t *)(base + lay.state));
 	if (f.done || w.overflow || w.n_hit == 0)
 		return; /* dsb_delete_small_A does not reach the build */
-	int dirs = dsb_hash_dirs(&w);
+	/* dsb_hash_dirs over the workgroup: the hits the scoring keeps (the first one from 200 on
+	 * scoring <= 50 ends them, at most 400), then their directions */
+	if (tid == 0) {
+		sh_n = w.n_hit;
+		sh_dirs = 0;
+	}
+	__syncthreads();
+	if (w.n_hit > 200)
+		for (uint32_t i = 200 + tid; i < w.n_hit; i += DSB_HL_WG)
+			if (w.hit[i].sum_score <= 50)
+				atomicMin(&sh_n, i);
+	__syncthreads();
+	uint32_t nh = DSB_MIN(400u, sh_n);
+	for (uint32_t i = tid; i < nh; i += DSB_HL_WG)
+		atomicOr(&sh_dirs, w.hit[i].direction == DSB_FORWARD ? 2u : 1u);
+	__syncthreads();
+	int dirs = (int)sh_dirs;
 	int c_dir = h == 0 ? 2 : 1; /* table 0: the forward hits' strand, table 1: the reverse hits' */
 	if ((c_dir & dirs) == 0)
 		return;
