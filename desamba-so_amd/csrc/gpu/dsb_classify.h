@@ -2624,6 +2624,70 @@ DSB_HD int dsb_hash_dirs(const dsb_read_ws *w)
 	return both_dir;
 }
 
+/* One strand of the read hash by one wave (the wave form of build_hash_table_M2's loop): chunks of
+ * 64 positions from the end; inside a chunk each lane finds the nearest higher lane with its key
+ * (its list successor) and whether a lower lane has it.  heads: 2^key_len entries (HBM in the
+ * scoring kernel, LDS in k_hash_lds), initialised here; lds_hb: DSB_HB_LDS bytes of LDS or 0. */
+DSB_HDN void dsb_hash_strand_w(const uint8_t *q, int n_pos, uint32_t *heads, uint32_t *node, int key_len, uint8_t *lds_hb,
+			       uint64_t *stats)
+{
+	uint32_t KEY_MASK = (1u << key_len) - 1;
+	uint32_t lane = dsb_lane();
+	for (uint32_t k = lane; k <= KEY_MASK; k += DSB_WV) heads[k] = DSB_HEMPTY;
+	dsb_wsync();
+	for (int cb = n_pos > 0 ? ((n_pos - 1) & ~(DSB_WV - 1)) : -1; cb >= 0; cb -= DSB_WV) {
+		int c_pos = cb + (int)lane;
+		int act = c_pos < n_pos;
+		uint32_t kmer = act ? dsb_q9mer(q + c_pos) : 0;
+		int key = act ? (int)(kmer & KEY_MASK) : -1 - (int)lane;
+		int has_prev = 0, nxt = -1;
+		if (lds_hb) {
+			/* every lane writes its id to a byte slot of its key's low bits and reads it
+			 * back: lanes sharing a key all lost, or lost to the one of them that won, so
+			 * walking the (few) losers and their winners finds every group */
+			uint8_t *hb = lds_hb + (key & (DSB_HB_LDS - 1));
+			if (act) *hb = (uint8_t)lane;
+			dsb_wsync();
+			int won = act ? (int)*hb : (int)lane;
+			uint64_t lost = dsb_wballot(won != (int)lane);
+			nxt = DSB_WV;
+			while (lost) {
+				int o = __builtin_ctzll(lost);
+				lost &= lost - 1;
+				int w2 = dsb_wshfl(won, o);
+				int k2 = dsb_wshfl(key, o), k3 = dsb_wshfl(key, w2);
+				if (k2 == key) {
+					if (o < (int)lane) has_prev = 1;
+					else if (o > (int)lane) nxt = DSB_MIN(nxt, o);
+				}
+				if (k3 == key) {
+					if (w2 < (int)lane) has_prev = 1;
+					else if (w2 > (int)lane) nxt = DSB_MIN(nxt, w2);
+				}
+			}
+			if (nxt == DSB_WV) nxt = -1;
+		} else {
+			for (int o = DSB_WV - 1; o >= 0; o--) {
+				int k2 = dsb_wshfl(key, o);
+				if (k2 == key) {
+					if (o < (int)lane) has_prev = 1;
+					else if (o > (int)lane) nxt = o;
+				}
+			}
+		}
+		uint32_t old = act ? heads[key] : DSB_HEMPTY;
+		uint32_t ent = dsb_hentry((uint32_t)c_pos, kmer, nxt >= 0 || old != DSB_HEMPTY, key_len);
+		uint32_t nent = (uint32_t)dsb_wshfl_any((int)ent, nxt >= 0 ? nxt : (int)lane);
+		if (act) {
+			if (stats) stats[DSB_ST_HASH_B] += 12;
+			node[c_pos] = nxt >= 0 ? nent : old;
+			if (!has_prev)
+				heads[key] = ent;
+		}
+		dsb_wsync();
+	}
+}
+
 /* build_hash_table_M2, src/cly.c:2168-2219: chained 9-mer hash of the read, per strand.
  * Lists hold positions in increasing order (the reference appends in position order), built
  * here from the last position backwards so that only the heads array is needed. */
@@ -2671,65 +2735,10 @@ DSB_HDN int dsb_build_hash_table(dsb_read_ws *w, int q_len)
 				heads[key] = dsb_hentry((uint32_t)c_pos, kmer, old != DSB_HEMPTY, key_len);
 			}
 		} else {
-			/* chunks of 64 positions from the end; inside a chunk each lane finds the nearest
-			 * higher lane with its key (its list successor) and whether a lower lane has it */
-			uint32_t lane = dsb_lane();
-			for (uint32_t k = lane; k <= KEY_MASK; k += DSB_WV) heads[k] = DSB_HEMPTY;
 			/* algorithmic bytes: the head table at the reference's key length (a longer key is an
-			 * implementation choice, not work), + 12 B per position below */
-			if (w->stats && lane == 0) w->stats[DSB_ST_HASH_B] += 4ull << dsb_hash_kl_ref((uint32_t)q_len);
-			dsb_wsync();
-			for (int cb = n_pos > 0 ? ((n_pos - 1) & ~(DSB_WV - 1)) : -1; cb >= 0; cb -= DSB_WV) {
-				int c_pos = cb + (int)lane;
-				int act = c_pos < n_pos;
-				uint32_t kmer = act ? dsb_q9mer(q + c_pos) : 0;
-				int key = act ? (int)(kmer & KEY_MASK) : -1 - (int)lane;
-				int has_prev = 0, nxt = -1;
-				if (w->lds_hb) {
-					/* every lane writes its id to a byte slot of its key's low bits and reads it
-					 * back: lanes sharing a key all lost, or lost to the one of them that won, so
-					 * walking the (few) losers and their winners finds every group */
-					uint8_t *hb = w->lds_hb + (key & (DSB_HB_LDS - 1));
-					if (act) *hb = (uint8_t)lane;
-					dsb_wsync();
-					int won = act ? (int)*hb : (int)lane;
-					uint64_t lost = dsb_wballot(won != (int)lane);
-					nxt = DSB_WV;
-					while (lost) {
-						int o = __builtin_ctzll(lost);
-						lost &= lost - 1;
-						int w2 = dsb_wshfl(won, o);
-						int k2 = dsb_wshfl(key, o), k3 = dsb_wshfl(key, w2);
-						if (k2 == key) {
-							if (o < (int)lane) has_prev = 1;
-							else if (o > (int)lane) nxt = DSB_MIN(nxt, o);
-						}
-						if (k3 == key) {
-							if (w2 < (int)lane) has_prev = 1;
-							else if (w2 > (int)lane) nxt = DSB_MIN(nxt, w2);
-						}
-					}
-					if (nxt == DSB_WV) nxt = -1;
-				} else {
-					for (int o = DSB_WV - 1; o >= 0; o--) {
-						int k2 = dsb_wshfl(key, o);
-						if (k2 == key) {
-							if (o < (int)lane) has_prev = 1;
-							else if (o > (int)lane) nxt = o;
-						}
-					}
-				}
-				uint32_t old = act ? heads[key] : DSB_HEMPTY;
-				uint32_t ent = dsb_hentry((uint32_t)c_pos, kmer, nxt >= 0 || old != DSB_HEMPTY, key_len);
-				uint32_t nent = (uint32_t)dsb_wshfl_any((int)ent, nxt >= 0 ? nxt : (int)lane);
-				if (act) {
-					if (w->stats) w->stats[DSB_ST_HASH_B] += 12;
-					node[c_pos] = nxt >= 0 ? nent : old;
-					if (!has_prev)
-						heads[key] = ent;
-				}
-				dsb_wsync();
-			}
+			 * implementation choice, not work), + 12 B per position */
+			if (w->stats && dsb_lane() == 0) w->stats[DSB_ST_HASH_B] += 4ull << dsb_hash_kl_ref((uint32_t)q_len);
+			dsb_hash_strand_w(q, n_pos, heads, node, key_len, w->lds_hb, w->stats);
 		}
 	}
 	return key_len;
