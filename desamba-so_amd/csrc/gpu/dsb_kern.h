@@ -357,28 +357,36 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 }
 
 /* The read 9-mer hash of the scoring phase (build_hash_table_M2, src/cly.c:2168-2219), built in
- * LDS by one wave per (read, strand) before the scoring launch (DSB_HASH_LDS):
+ * LDS by a workgroup of 256 lanes per (read, strand) before the scoring launch (DSB_HASH_LDS):
  * the scoring kernel's own build updated its head table in HBM, a scattered 4-B read-modify-
  * write per position (~1 G per 100k reads, 32-B write granules), and building the tables twice
  * there cost ~20 ms per 100k-read chunk on the C2 proxy (profiles/r04_d).  Here the head table
  * (2^14 keys, dsb_hash_kl_lds) lives in LDS while the positions are inserted, and goes to HBM once,
  * coalesced; the node entries are written as before (consecutive positions, coalesced).
  *
- * The insertion is the scoring kernel's own wave build (dsb_hash_strand_w: blocks of 64 positions
- * from the end, key groups found through LDS lane-id slots and wave shuffles) with the head table
- * in LDS: no barrier across waves, 36 KB of LDS per wave at key length 13.  A first form with 256
- * lanes per strand spent its time in the cross-wave barriers and the serial walk of the lost
- * lanes through LDS (91 / 52 ms per 300k reads at key length 14 / 13, profiles/r04_g). */
-#define DSB_HL_WG 64
+ * Positions are inserted from the end in blocks of 256 (one per lane), so every list keeps
+ * increasing positions.  Inside a block each lane must find the nearest higher lane with its key
+ * (its list successor) and whether a lower lane has it (then that lane, not this one, becomes the
+ * head): every lane writes its lane id to a byte slot of its key's low bits and reads it back; two
+ * lanes with one key wrote the same slot, so at least one of them lost, and the lost lanes (a few
+ * per block) with the lanes they lost to are all the candidates a lane has to compare with (the
+ * wave build's argument, dsb_build_hash_table). */
+#define DSB_HL_WG 256
+static_assert(DSB_HASH_LDS_KL <= 16, "k_hash_lds keeps keys in 16 bits");
+#define DSB_HL_SLOTS 4096
 template <int STATS>
-__global__ __launch_bounds__(DSB_HL_WG) void k_hash_lds(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
-						   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
-						   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
-						   unsigned long long *__restrict__ gstats)
+__global__ __launch_bounds__(DSB_HL_WG, DSB_HASH_LDS_KL <= 13 ? 4 : 2) void k_hash_lds(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+							 const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+							 uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
+							 unsigned long long *__restrict__ gstats)
 {
 	__shared__ uint32_t heads[1u << DSB_HASH_LDS_KL];
-	__shared__ uint8_t hb[DSB_HB_LDS];
-	uint32_t t = blockIdx.x >> 1, h = blockIdx.x & 1, lane = threadIdx.x;
+	__shared__ uint8_t slot[DSB_HL_SLOTS];
+	__shared__ uint16_t keyl[DSB_HL_WG]; /* the lanes' keys (< 2^14) */
+	__shared__ uint32_t entl[DSB_HL_WG];
+	__shared__ uint2 los[DSB_HL_WG]; /* lost lane | winner << 8 | its key << 16, the winner's key */
+	__shared__ uint32_t n_los, sh_n, sh_dirs;
+	uint32_t t = blockIdx.x >> 1, h = blockIdx.x & 1, tid = threadIdx.x;
 	if (t >= n)
 		return;
 	uint32_t r = order[t];
@@ -394,25 +402,23 @@ __global__ __launch_bounds__(DSB_HL_WG) void k_hash_lds(const dsb_dindex_t *__re
 	dsb_state_load(&w, &f, (const dsb_rstate_t *)(base + lay.state));
 	if (f.done || w.overflow || w.n_hit == 0)
 		return; /* dsb_delete_small_A does not reach the build */
-	/* dsb_hash_dirs over the wave: the hits the scoring keeps (the first one from 200 on scoring
-	 * <= 50 ends them, at most 400), then their directions, 64 hits per round trip */
-	uint32_t nh = w.n_hit;
-	if (nh > 200)
-		for (uint32_t gb = 200; gb < w.n_hit; gb += DSB_WV) {
-			uint32_t i = gb + lane;
-			uint64_t m = __ballot(i < w.n_hit && w.hit[i].sum_score <= 50);
-			if (m) {
-				nh = gb + (uint32_t)__builtin_ctzll(m);
-				break;
-			}
-		}
-	nh = DSB_MIN(400u, nh);
-	int dirs = 0;
-	for (uint32_t gb = 0; gb < nh && dirs != 3; gb += DSB_WV) {
-		uint32_t i = gb + lane;
-		int d = i < nh ? (w.hit[i].direction == DSB_FORWARD ? 2 : 1) : 0;
-		dirs |= (__ballot(d == 2) ? 2 : 0) | (__ballot(d == 1) ? 1 : 0);
+	/* dsb_hash_dirs over the workgroup: the hits the scoring keeps (the first one from 200 on
+	 * scoring <= 50 ends them, at most 400), then their directions */
+	if (tid == 0) {
+		sh_n = w.n_hit;
+		sh_dirs = 0;
 	}
+	__syncthreads();
+	if (w.n_hit > 200)
+		for (uint32_t i = 200 + tid; i < w.n_hit; i += DSB_HL_WG)
+			if (w.hit[i].sum_score <= 50)
+				atomicMin(&sh_n, i);
+	__syncthreads();
+	uint32_t nh = DSB_MIN(400u, sh_n);
+	for (uint32_t i = tid; i < nh; i += DSB_HL_WG)
+		atomicOr(&sh_dirs, w.hit[i].direction == DSB_FORWARD ? 2u : 1u);
+	__syncthreads();
+	int dirs = (int)sh_dirs;
 	int c_dir = h == 0 ? 2 : 1; /* table 0: the forward hits' strand, table 1: the reverse hits' */
 	if ((c_dir & dirs) == 0)
 		return;
@@ -420,13 +426,71 @@ __global__ __launch_bounds__(DSB_HL_WG) void k_hash_lds(const dsb_dindex_t *__re
 	const dsb_sdir_t *csd = (w.sd[0].direction == direction) ? &w.sd[0] : &w.sd[1];
 	const uint8_t *q = w.bin + (csd->strand ? L : 0);
 	int kl = dsb_hash_kl_lds(L);
+	uint32_t KEY_MASK = (1u << kl) - 1;
+	uint32_t *g_heads = w.hh[h], *node = w.hn[h];
 	int n_pos = (int)L - DSB_S_A_KMER_L + 1;
-	dsb_hash_strand_w(q, n_pos, heads, w.hn[h], kl, hb, nullptr);
-	uint32_t *g_heads = w.hh[h];
-	for (uint32_t k = lane; k < (1u << kl); k += DSB_WV) g_heads[k] = heads[k];
-	if (STATS && lane == 0) /* head table at the reference's key length + 12 B per position */
-		atomicAdd(gstats + DSB_ST_STRIDE * DSB_PH_DELA + DSB_ST_HASH_B,
-			  (unsigned long long)(4ull * (1ull << dsb_hash_kl_ref(L)) + 12ull * n_pos));
+	for (uint32_t k = tid; k <= KEY_MASK; k += DSB_HL_WG) heads[k] = DSB_HEMPTY;
+	if (STATS && tid == 0) {
+		unsigned long long *st = gstats + DSB_ST_STRIDE * DSB_PH_DELA;
+		/* head table at the reference's key length + per position: the node write, head read and write */
+		atomicAdd(st + DSB_ST_HASH_B, (unsigned long long)(4ull * (1ull << dsb_hash_kl_ref(L)) + 12ull * n_pos));
+	}
+	/* the blocks' k-mers, loaded four blocks ahead (a block's LDS work is shorter than a load) */
+	int cb = (n_pos - 1) & ~(DSB_HL_WG - 1);
+	auto ld = [&](int b) -> uint32_t { return (b >= 0 && b + (int)tid < n_pos) ? dsb_q9mer(q + b + tid) : 0; };
+	uint32_t k0 = ld(cb), k1 = ld(cb - DSB_HL_WG), k2 = ld(cb - 2 * DSB_HL_WG), k3 = ld(cb - 3 * DSB_HL_WG);
+	__syncthreads();
+	for (; cb >= 0; cb -= DSB_HL_WG) {
+		int c_pos = cb + (int)tid;
+		int act = c_pos < n_pos;
+		uint32_t km = k0;
+		k0 = k1;
+		k1 = k2;
+		k2 = k3;
+		k3 = ld(cb - 4 * DSB_HL_WG);
+		int key = act ? (int)(km & KEY_MASK) : -1 - (int)tid;
+		keyl[tid] = (uint16_t)key; /* read back for active (winning) lanes only */
+		if (tid == 0)
+			n_los = 0;
+		if (act)
+			slot[key & (DSB_HL_SLOTS - 1)] = (uint8_t)tid;
+		__syncthreads();
+		int won = act ? (int)slot[key & (DSB_HL_SLOTS - 1)] : (int)tid;
+		if (won != (int)tid) {
+			uint32_t k = atomicAdd(&n_los, 1u);
+			los[k] = make_uint2(tid | ((uint32_t)won << 8) | ((uint32_t)key << 16), keyl[won]);
+		}
+		__syncthreads();
+		int has_prev = 0, nxt = DSB_HL_WG;
+		uint32_t nl = n_los;
+		if (act)
+			for (uint32_t k = 0; k < nl; k++) {
+				uint2 e = los[k]; /* one 8-B LDS read per lost lane, independent of the others */
+				int o = (int)(e.x & 0xffu), w2 = (int)((e.x >> 8) & 0xffu);
+				if ((int)(e.x >> 16) == key) {
+					if (o < (int)tid) has_prev = 1;
+					else if (o > (int)tid) nxt = DSB_MIN(nxt, o);
+				}
+				if ((int)e.y == key) {
+					if (w2 < (int)tid) has_prev = 1;
+					else if (w2 > (int)tid) nxt = DSB_MIN(nxt, w2);
+				}
+			}
+		uint32_t old = act ? heads[key] : DSB_HEMPTY;
+		uint32_t ent = dsb_hentry((uint32_t)c_pos, km, nxt < DSB_HL_WG || old != DSB_HEMPTY, kl);
+		entl[tid] = ent;
+		__syncthreads();
+		if (act) {
+			node[c_pos] = nxt < DSB_HL_WG ? entl[nxt] : old;
+			if (!has_prev)
+				heads[key] = ent;
+		}
+		/* no barrier here: the next block's first LDS writes (keys, slots, the loser count) touch
+		 * nothing this block reads after the barrier above, and its head reads follow its own
+		 * first barrier */
+	}
+	__syncthreads();
+	for (uint32_t k = tid; k <= KEY_MASK; k += DSB_HL_WG) g_heads[k] = heads[k];
 }
 
 /* One read of a phase of part A with one wavefront per read (dsb_wave.h): fast seeding
