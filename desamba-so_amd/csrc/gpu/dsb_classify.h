@@ -2583,7 +2583,7 @@ DSB_HD int dsb_hash_kl(uint32_t q_len)
  * a 2^14-entry head table (64 KB of LDS) holds the key of every read up to 2^23 positions; the
  * key length is not observable (above), so reads whose dsb_hash_kl is longer use 14 bits. */
 #ifndef DSB_HASH_LDS
-#define DSB_HASH_LDS 0
+#define DSB_HASH_LDS 1 /* measured (C2, 300k reads): 609.8k -> 632.5k reads/s (profiles/r04_i) */
 #endif
 #ifndef DSB_HASH_LDS_KL
 #define DSB_HASH_LDS_KL 13 /* measured (C2, 300k reads): key length 12 / 13 / 14 -> hash build 39 / 52 / 91 ms, scoring 197 / 169 / 157 ms */
