@@ -5,7 +5,8 @@ WRITE_SIZE in the other; they cannot share a pass on gfx950) over the same bench
     python tools/traffic_json.py gpurun_out/TAG WORKLOAD READS KERNEL_PREFIX PROFILE_TAG
 
 Per launch of the kernel (KERNEL_PREFIX, e.g. "k_wave_phase<8"): FETCH_SIZE and WRITE_SIZE (KB)
-summed over its dispatches / the number of dispatches; hbm_bytes_per_launch = 2 x FETCH + WRITE
+summed over its dispatches of >= 1000 workgroups (the chunk launches the bench's HIP events time;
+an overflow re-run of a few reads is a small launch) / the number of those dispatches; hbm_bytes_per_launch = 2 x FETCH + WRITE
 (MI355X_MICROARCH.md: gfx950's FETCH_SIZE counts half of a streaming read's bytes), and the
 random-access reading FETCH + WRITE (profiles/r03_calib: a random 4-B load is one 64-B unit and
 FETCH_SIZE counts it whole) as hbm_bytes_per_launch_calibrated.
@@ -17,7 +18,7 @@ import sqlite3
 import sys
 
 
-def per_launch(pass_dir, counter, prefix):
+def per_launch(pass_dir, counter, prefix, min_grid=1000):
     dbs = glob.glob(f"{pass_dir}/**/*.db", recursive=True)
     if not dbs:
         raise SystemExit(f"no rocprofv3 database under {pass_dir}")
@@ -25,10 +26,13 @@ def per_launch(pass_dir, counter, prefix):
     cols = [r[1] for r in db.execute("pragma table_info(counters_collection)")]
     did = "dispatch_id" if "dispatch_id" in cols else None
     tot, disp, name = 0.0, set(), None
-    q = f"select kernel_name, counter_name, value{', ' + did if did else ''} from counters_collection"
+    q = (f"select kernel_name, counter_name, value, grid_size, workgroup_size{', ' + did if did else ''} "
+         "from counters_collection")
     n_rows = 0
     for row in db.execute(q):
         k, c, v = row[0], row[1], row[2]
+        if row[3] // max(1, row[4]) < min_grid:  # an overflow re-run of a few reads, not a chunk launch
+            continue
         m = re.match(r"(?:void )?([\w:]+(?:<[^>]*>)?)", k)
         k = m.group(1) if m else k
         if not k.startswith(prefix) or c != counter:
@@ -37,7 +41,7 @@ def per_launch(pass_dir, counter, prefix):
         tot += v
         n_rows += 1
         if did:
-            disp.add(row[3])
+            disp.add(row[5])
     n = len(disp) if did else n_rows
     return name, tot / max(1, n), n
 
