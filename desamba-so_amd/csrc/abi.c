@@ -360,11 +360,9 @@ void dsb_batch_free(void *idx, dsb_batch *b)
 int dsb_parse_dump(const char *text, uint64_t text_n, int slow, uint64_t batch_reads, char **output,
 		   uint64_t *output_n)
 {
-	if (slow)
-		setenv("DSB_PARSE_SLOW", "1", 1);
 	dsb_parser *p = dsb_parser_new(text, text_n);
-	if (slow)
-		unsetenv("DSB_PARSE_SLOW");
+	if (slow) /* a parser field, not the process environment other library threads read */
+		dsb_parser_set_fast(p, 0);
 	dsb_reads_t r;
 	memset(&r, 0, sizeof(r));
 	dsb_str out = {0, 0, 0};
@@ -390,6 +388,11 @@ int dsb_parse_dump(const char *text, uint64_t text_n, int slow, uint64_t batch_r
 	*output_n = out.l;
 	*output = out.s ? out.s : calloc(1, 1);
 	return 0;
+}
+
+uint64_t dsb_timing_size(void)
+{
+	return sizeof(dsb_timing_t);
 }
 
 const char *dsb_version(void)

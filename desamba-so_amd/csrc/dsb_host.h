@@ -98,6 +98,7 @@ int dsb_parse_reads(const char *buf, uint64_t len, dsb_reads_t *out);
  * records appended (0: end of input).  Records stay valid until dsb_parser_free. */
 typedef struct dsb_parser dsb_parser;
 dsb_parser *dsb_parser_new(const char *buf, uint64_t len);
+void dsb_parser_set_fast(dsb_parser *p, int fast);
 uint64_t dsb_parser_next(dsb_parser *p, dsb_reads_t *out, uint64_t max_reads, uint64_t max_bases);
 void dsb_parser_stats(const dsb_parser *p, uint64_t *n_fast, uint64_t *n_slow);
 void dsb_parser_free(dsb_parser *p);

@@ -281,6 +281,12 @@ dsb_parser *dsb_parser_new(const char *buf, uint64_t len)
 	return p;
 }
 
+/* the zero-copy fast path on (1) or off (0: every record through the byte-level kseq emulation) */
+void dsb_parser_set_fast(dsb_parser *p, int fast)
+{
+	p->fast = fast;
+}
+
 static void reads_push(dsb_reads_t *out, const dsb_rec_t *r)
 {
 	if (out->n == out->m) {

@@ -123,7 +123,7 @@ typedef struct {
 	/* optional counters for algorithmic-byte accounting (bench) */
 	uint64_t *stats;
 	uint32_t dbg;           /* diagnostics: force sequential variants of the wave loops */
-	uint32_t launch_tag;    /* unique per kernel launch (host counter, never 0): seeding sp_set slot tags */
+	uint64_t launch_tag;    /* unique per kernel launch (host counter, never 0, < 2^40): seeding sp_set slot tags */
 	uint64_t *tmr;          /* timer kernels: wave clocks per DSB_ST_T_* slot (LDS, lane 0), or 0 */
 } dsb_read_ws;
 
@@ -563,25 +563,27 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_spset_t *s) { return dsb_spset_inse
  * The same set as an open-addressing hash (one per lane of the wave-cooperative seeding):
  * membership == "inserted since the last reset or since the last wrap of the reference's
  * 500-entry array" (a wrap is `l == m -> l = 0`, i.e. the array forgets everything), so a
- * generation counter replaces clearing.  A slot is {node, gen64}: gen64 = the launch tag << 32 |
- * the lane's generation.  Launch tags only grow within a process, so slots written by earlier
- * launches never compare equal and read as empty: the table is never cleared (kernels.hip
- * clears the workspace if the 32-bit tag counter ever wraps).  Within one launch a lane's
- * generation holds at most 500 entries (the reference's wrap), so a probe always finds a slot
- * of another generation among the 512.
+ * generation counter replaces clearing.  A slot is {node, gen64}: gen64 = the launch tag << 24 |
+ * the lane's generation (24 bits: a lane starts far fewer generations in one launch).  Launch
+ * tags come from one 64-bit counter for the whole process (every context of every GPU) and never
+ * repeat below 2^40, so slots written by earlier launches — of any context whose workspace bytes
+ * these are — never compare equal and read as empty: the table is never cleared.  Within one
+ * launch a lane's generation holds at most 500 entries (the reference's wrap), so a probe always
+ * finds a slot of another generation among the 512.
  */
 #ifndef DSB_HSET_LOG2
 #define DSB_HSET_LOG2 9
 #endif
 #define DSB_HSET_SLOTS (1u << DSB_HSET_LOG2) /* > 500: the reference's set never holds more */
 #define DSB_HSET_SLOT_U64 2
+#define DSB_HSET_GEN_BITS 24
 typedef struct { uint64_t *tab; uint32_t stride, gen; int l, m; uint64_t tag; } dsb_hset_t;
 /* slot tag: the launch's tag (a host counter bumped for every phase launch, so two launches —
  * FAST0/FAST1, SLOW0/SLOW1, later chunks reusing the same workspace bytes, overflow re-runs —
  * never share one) in the high word, the lane's generation in the low word */
 DSB_HD uint64_t dsb_hset_tag(const dsb_read_ws *w)
 {
-	return (uint64_t)w->launch_tag << 32;
+	return w->launch_tag << DSB_HSET_GEN_BITS;
 }
 DSB_HD void dsb_set_reset(dsb_hset_t *s)
 {
@@ -598,7 +600,7 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_hset_t *s)
 		s->gen++;
 	}
 	uint32_t h = (uint32_t)((node * 0x9E3779B97F4A7C15ull) >> (64 - DSB_HSET_LOG2));
-	uint64_t g = s->tag | s->gen;
+	uint64_t g = s->tag | (s->gen & ((1u << DSB_HSET_GEN_BITS) - 1));
 	for (;;) {
 		uint64_t *slot = s->tab + (uint64_t)h * s->stride;
 		uint64_t sn = slot[0], sg = slot[1];

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_phase(const dsb_dindex_t 
 					       uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 					       dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
 					       unsigned long long *__restrict__ gstats, uint32_t dbg,
-									      uint32_t tag)
+									      uint64_t tag)
 {
 	(void)dbg;
 	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 							   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 							   dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
 							   unsigned long long *__restrict__ gstats, uint32_t dbg,
-									      uint32_t tag)
+									      uint64_t tag)
 {
 	(void)dbg; (void)ro; (void)n_overflow; (void)gstats; (void)tag;
 	uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 								   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
 								   uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 								   dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
-								   unsigned long long *__restrict__ gstats, uint32_t dbg, uint32_t tag)
+								   unsigned long long *__restrict__ gstats, uint32_t dbg, uint64_t tag)
 {
 	static_assert(G >= 4 && G <= 32 && (G & (G - 1)) == 0, "lanes per strand: 4, 8, 16 or 32");
 	/* positions per grid / run batch (<= G lanes) */
@@ -502,7 +502,7 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 						uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t t,
 						dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
 						uint64_t *st, uint64_t *tmr_lds, unsigned long long *__restrict__ gstats,
-						uint32_t dbg, uint32_t tag)
+						uint32_t dbg, uint64_t tag)
 {
 	const int ph = PH;
 	uint32_t lane = threadIdx.x;
@@ -597,7 +597,7 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 						    uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t n,
 						    dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
 						    unsigned long long *__restrict__ gstats, uint32_t dbg,
-									      uint32_t tag)
+									      uint64_t tag)
 {
 	uint32_t lane = threadIdx.x;
 	uint64_t st[DSB_ST_N];
@@ -625,5 +625,5 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 /* launch signature shared by the lane (k_phase) and wave (k_wave_phase) phase kernels */
 typedef void (*dsb_phase_fn)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
 			     const uint32_t *, uint32_t, dsb_read_out_t *, uint32_t *, unsigned long long *, uint32_t,
-			     uint32_t);
+			     uint64_t);
 #endif

@@ -272,7 +272,8 @@ struct dsb_gpu_dev {
 	dbuf vlen, vso, vidx, vtid; /* the deferred overflow re-runs of a batch (batch_run) */
 	hipEvent_t evh[2][2];    /* k_hash_lds before the scoring launch, per stream (launch_phase) */
 	int evh_used[2] = {0, 0};
-	uint32_t tag = 0;        /* tag of this context's last phase launch (dsb_hset_tag; next_launch_tag) */
+	uint64_t tag = 0;        /* tag of this context's last phase launch (dsb_hset_tag; next_launch_tag) */
+	uint64_t tag_ctx = 0;    /* DSB_TEST_TAG_PER_CTX: round 3's per-context counter (tests only) */
 	/* streamed batches (read_classify pipeline): uploads on their own stream through pinned
 	 * staging, under their own lock, beside the kernels of the batch before */
 	hipStream_t cstream;
@@ -619,8 +620,28 @@ static uint32_t wave_phases(void)
  * cleared, so a tag must never repeat on workspace bytes: one counter for the whole process
  * (every context of every GPU: a context's workspace may be re-allocated over bytes another
  * context wrote), and workspace buffers are zero-filled when allocated (tag 0 is never used). */
-static std::atomic<uint32_t> g_launch_tag{0};
-static uint32_t next_launch_tag(void) { return ++g_launch_tag; }
+static std::atomic<uint64_t> g_launch_tag{0};
+static uint64_t next_launch_tag(void) { return ++g_launch_tag; }
+
+/* Test knobs for the tag-collision regression test (tests/test_gpu_parity.py): DSB_TEST_SHARED_WS=1
+ * gives every context of the process one chunk workspace (runs serialised by a process-wide lock,
+ * no zero fill between contexts: each context's launches meet the slots the others left), and
+ * DSB_TEST_TAG_PER_CTX=1 brings back round 3's per-context tag counters, so that the test can show
+ * it detects the collision the process-wide counter prevents. */
+static int test_env(const char *name)
+{
+	const char *e = getenv(name);
+	return e && atoi(e) != 0;
+}
+struct shared_ws_t {
+	pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+	dbuf ws;
+};
+static shared_ws_t *shared_ws(void)
+{
+	static shared_ws_t *s = new shared_ws_t(); /* never freed: lives as long as the process */
+	return s;
+}
 
 /* the LDS read-hash build's time (ms_phase[DSB_PH_HASH]) since the last call, taken out of the
  * scoring phase's (the callers time the hash build + scoring launch pair together); the events
@@ -655,16 +676,12 @@ static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, 
 	uint32_t dbg = wave_dbg();
 	/* every launch gets its own slot tag; if the 32-bit counter ever wraps, the workspace is
 	 * cleared once (both streams drained) so that no slot of an earlier launch can match */
-	if ((g->tag = next_launch_tag()) == 0) {
-		hipDeviceSynchronize();
-		g->tag = next_launch_tag();
-		if (g->ws.p)
-			hipMemsetAsync(g->ws.p, 0, g->ws.cap, s);
-		if (g->wsr.p) /* the retry buffer holds tagged sp_set slots too */
-			hipMemsetAsync(g->wsr.p, 0, g->wsr.cap, s);
-		hipStreamSynchronize(s);
+	g->tag = test_env("DSB_TEST_TAG_PER_CTX") ? ++g->tag_ctx : next_launch_tag();
+	if (g->tag >= (1ull << (64 - DSB_HSET_GEN_BITS))) { /* 2^40 launches: unreachable in practice */
+		fprintf(stderr, "[dsb] launch tag space exhausted; reload the index\n");
+		abort();
 	}
-	uint32_t tag = g->tag;
+	uint64_t tag = g->tag;
 	if (ph == DSB_PH_DELA && DSB_HASH_LDS && m) {
 		/* the read hash in LDS (k_hash_lds), then the scoring; timed apart by hash_ms() */
 		int si = s == g->stream2;
@@ -940,6 +957,15 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		     dsb_gpu_timing &T, char *err, size_t errn, const dsb_carry_hooks *hooks = nullptr)
 {
 	double hs[HS_N] = {0}, hs_t = now_ms();
+	/* DSB_TEST_SHARED_WS (tests): one chunk workspace for every context, runs serialised */
+	shared_ws_t *sw = test_env("DSB_TEST_SHARED_WS") ? shared_ws() : nullptr;
+	struct unlock_t {
+		shared_ws_t *sw;
+		~unlock_t() { if (sw) pthread_mutex_unlock(&sw->mu); }
+	} unlock_sw = {sw};
+	if (sw)
+		pthread_mutex_lock(&sw->mu);
+	dbuf &WS = sw ? sw->ws : g->ws;
 	auto hs_mark = [&](int k) {
 		double t = now_ms();
 		hs[k] += t - hs_t;
@@ -1094,12 +1120,12 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		T.n_chunks++;
 		hs_mark(HS_SIZE);
 		uint64_t rused = 0; /* bytes of the retry buffer holding this chunk's re-run reads */
-		void *ws_before = g->ws.p;
-		if (g->ws.ensure(ws_total + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
+		void *ws_before = WS.p;
+		if (WS.ensure(ws_total + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
 		    g->word_off.ensure(8 * (size_t)cn + 16, err, errn))
 			return -1;
-		if (g->ws.p != ws_before) /* fresh bytes: no stale sp_set slot may carry a live tag */
-			HIP_OK(hipMemsetAsync(g->ws.p, 0, g->ws.cap, s));
+		if (WS.p != ws_before) /* fresh bytes: no stale sp_set slot may carry a live tag */
+			HIP_OK(hipMemsetAsync(WS.p, 0, WS.cap, s));
 		HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
 		HIP_OK(hipMemcpyAsync(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
 		const uint32_t *cl = b->d_len.as<uint32_t>() + cb;
@@ -1107,7 +1133,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		/* length-sorted order (longest first) for the one-lane-per-read kernels */
 		const std::vector<uint32_t> &order = chunk_order(b, cb, ce);
 		HIP_OK(hipMemcpyAsync(g->order.p, order.data(), 4ull * cn, hipMemcpyHostToDevice, s));
-		uint8_t *wsb = g->ws.as<uint8_t>();
+		uint8_t *wsb = WS.as<uint8_t>();
 		hs_mark(HS_SETUP);
 		hipEventRecord(g->ev_a, s);
 		k_encode<<<cn, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, nullptr, cn);
@@ -1372,7 +1398,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		HIP_OK(hipMemcpy(g->vso.p, vso.data(), 8ull * m, hipMemcpyHostToDevice));
 		HIP_OK(hipMemcpy(g->vidx.p, vidx.data(), 4ull * m, hipMemcpyHostToDevice));
 		uint64_t rused = 0;
-		uint8_t *wsb = g->ws.as<uint8_t>();
+		uint8_t *wsb = WS.as<uint8_t>();
 		const uint32_t *vcl = g->vlen.as<uint32_t>();
 		if (retry_view(m, 0, vlen, vscale, vws, vro, vcl, g->vso.as<uint64_t>(), wsb, rused, m))
 			return -1;

@@ -43,7 +43,7 @@ typedef struct pbatch {
 typedef struct {
 	dsb_index *ix;
 	dsb_pool *pool;
-	int format, max_sec_N, stats_on, n_dev;
+	int format, max_sec_N, stats_on, n_dev, round_robin;
 	pthread_mutex_t mu;
 	pthread_cond_t cv;
 	pbatch *parsed_head, *parsed_tail;       /* parsed, not yet staged */
@@ -207,8 +207,10 @@ static void *stager(void *arg)
 	char err[512];
 	for (;;) {
 		pthread_mutex_lock(&p->mu);
-		/* at most two batches per GPU between staging and classified: one classifying, one staged */
-		while (!p->failed && (p->runq_n[slot] >= 2 || (!p->parsed_head && !p->parse_done)))
+		/* at most two batches per GPU between staging and classified: one classifying, one staged;
+		 * DSB_TEST_ROUND_ROBIN (tests): batch k goes to GPU context k mod n */
+		while (!p->failed && (p->runq_n[slot] >= 2 || (!p->parsed_head && !p->parse_done) ||
+				      (p->round_robin && p->parsed_head && p->parsed_head->seq % (uint64_t)p->n_dev != (uint64_t)slot)))
 			pthread_cond_wait(&p->cv, &p->mu);
 		if (p->failed || !p->parsed_head) {
 			p->stagers_done++;
@@ -481,6 +483,7 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 	p->carry0 = *max_read_l;
 	pthread_mutex_init(&p->mu, NULL);
 	pthread_cond_init(&p->cv, NULL);
+	p->round_robin = env_u64("DSB_TEST_ROUND_ROBIN", 0) != 0;
 	p->max_reads = env_u64("DSB_PIPE_READS", 100000); /* measured (C2 proxy, 100k reads): 25k / 50k / 100k -> 278k / 292k / 317k reads/s */
 	p->max_bases = env_u64("DSB_PIPE_MBP", 400) * 1000000ull;
 	p->depth = env_u64("DSB_PIPE_DEPTH", 2 + 2 * (uint64_t)n_dev);

@@ -94,6 +94,10 @@ def lib(path: str | None = None):
     L.dsb_parse_dump.argtypes = [C.c_char_p, u64, C.c_int, u64, C.POINTER(C.c_void_p), u64p]
     L.dsb_parse_dump.restype = C.c_int
     L.dsb_version.restype = C.c_char_p
+    L.dsb_timing_size.restype = C.c_uint64
+    if L.dsb_timing_size() != C.sizeof(Timing):  # the binding mirrors include/desamba_mi355x.h
+        raise RuntimeError(f"{p}: dsb_timing_t is {L.dsb_timing_size()} bytes, this binding's Timing "
+                           f"{C.sizeof(Timing)}: rebuild the library or update pydesamba.Timing")
     L.dsb_device_count.restype = C.c_int
     L.dsb_free.argtypes = [vp]
     L.dsb_unload_index.argtypes = [vp]

@@ -70,6 +70,9 @@ int dsb_parse_dump(const char *text, uint64_t text_n, int slow, uint64_t batch_r
 		   uint64_t *output_n);
 
 const char *dsb_version(void);
+/* sizeof(dsb_timing_t) as this library fills it: a caller built against another version of this
+ * header checks it before passing a timing struct (the struct has grown between versions) */
+uint64_t dsb_timing_size(void);
 int dsb_device_count(void);
 void dsb_free(void *p);
 void dsb_unload_index(void *idx);

@@ -161,6 +161,49 @@ def test_concurrent_multi_batch_calls_share_contexts_without_deadlock(gpu_index)
     assert serial[0] == golden("mixed.herm.sam_full")
 
 
+def test_sp_set_tags_never_collide_across_contexts(pyd, fixture_index):
+    """Regression test for round 3's lost-anchor race: the seeding sp_set slots are never cleared
+    and match only the tag of the launch that wrote them, so a tag must never repeat on the same
+    workspace bytes, whichever context wrote them (kernels.hip next_launch_tag).  Deterministic
+    form: one chunk workspace for both contexts of DSB_DEVICES=0,0 (DSB_TEST_SHARED_WS), and the
+    same reads run first on one context and then again, at the same workspace offsets, on the other
+    (batch 0 = X on context 0, batch 1 = X X X X on context 1: DSB_PIPE_READS = 4 |X|, the first
+    batch being a quarter, DSB_TEST_ROUND_ROBIN for the batch-to-context order).  Every copy of X must give X's records.  With round 3's per-context
+    tag counters (DSB_TEST_TAG_PER_CTX) context 1's launches reuse context 0's tags over the same
+    sp_set slots and drop rows, which this test detects."""
+    lines = golden("ont.fq").split(b"\n")
+    x = b"\n".join(lines[:800]) + b"\n"  # the first 200 four-line records
+    assert x.count(b"\n+\n") == 200
+    data = x * 5
+    env = {"DSB_DEVICES": "0,0", "DSB_GPU_CONTEXTS": "1", "DSB_PIPE_READS": "800", "DSB_TEST_SHARED_WS": "1",
+           "DSB_TEST_ROUND_ROBIN": "1"}
+
+    def run(extra):
+        os.environ.update(env)
+        os.environ.update(extra)
+        try:
+            idx = pyd.Index(fixture_index)
+            try:
+                assert idx.devices() == [0, 0]
+                out, t, _ = idx.classify(data, fmt=pyd.FMT_SAM)
+                assert t["n_batches"] == 2 and t["n_devices"] == 2
+                return groups(out)
+            finally:
+                idx.close()
+        finally:
+            for k in list(env) + list(extra):
+                os.environ.pop(k, None)
+
+    g = run({})
+    assert len(g) == 1000
+    first = g[:200]
+    for c in range(1, 5):
+        assert g[200 * c:200 * (c + 1)] == first, f"copy {c} of the reads differs"
+    bad = run({"DSB_TEST_TAG_PER_CTX": "1"})
+    assert any(bad[200 * c:200 * (c + 1)] != bad[:200] for c in range(1, 5)), \
+        "per-context tags over shared workspace bytes should drop rows: the test would not detect the race"
+
+
 def test_two_calls_carry_pool_state_like_one_call(gpu_index, pyd):
     """max_read_l persists per thread_id across read_classify calls (src/cly.c:2953)."""
     fq = golden("mixed.fq")

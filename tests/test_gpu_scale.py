@@ -181,6 +181,33 @@ def test_ekmer_table_sizes_match_reference(pyd, c1_dir, tmp_path_factory, tmp_pa
         shutil.rmtree(d, ignore_errors=True)
 
 
+def test_reads_over_65kb_match_reference(pyd, c1_dir, tmp_path):
+    """Reads of 66-100 kb (C4's ONT tail): the reference's read buffer
+    realloc(NULL, 2L + 20) (BUFF_REALLOC, src/lib/utils.h:117-122) is then above glibc's 128 KB
+    mmap threshold, so the 8 bytes in front of the forward read are an mmapped chunk's header, not
+    the heap chunk header dsb_chunk_header models; they matter only to a backward extension that
+    runs past the read's first base into them.  These reads also take the 2^17-2^18-key read hashes
+    of the reference (and the LDS build's 2^13 keys here).  T1 / T2 on every read, T3 bounded,
+    against the hermetic reference, with the long reads interleaved among 8 kb ones."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import simulate
+    seed = int(os.environ.get("DSB_TEST_SEED", 9191 + int.from_bytes(os.urandom(2), "little")))
+    genomes = simulate.read_fasta_genomes_from_index(c1_dir)
+    longs = list(simulate.simulate_reads(genomes, 40, seed, "ont", 80000, min_len=66000, max_len=100000))
+    shorts = list(simulate.simulate_reads(genomes, 200, seed + 1, "ont", 8000))
+    reads = []
+    for i, r in enumerate(shorts):
+        reads.append(r)
+        if i % 5 == 4 and longs:
+            reads.append(longs.pop())
+    reads.extend(longs)
+    lens = [len(r[1]) for r in reads]
+    assert sum(L >= 65526 for L in lens) >= 30, sorted(lens)[-5:]  # 2L + 20 >= 128 KB
+    fq = tmp_path / f"long_{seed}.fq"
+    simulate.write_fastq(reads, str(fq))
+    _check_vs_reference(pyd, c1_dir, fq, seed, "C1-reads-over-65kb")
+
+
 def test_c4_mix_150bp_20kb_interleaved_matches_reference(pyd, c1_dir, tmp_path):
     seed = int(os.environ.get("DSB_TEST_SEED", 6161 + int.from_bytes(os.urandom(2), "little")))
     fq = _sim(c1_dir, tmp_path, 1000, seed, "c4")
