@@ -369,37 +369,45 @@ DSB_HD void dsb_isl_init(dsb_isl_t *s, int nk, int fwd, int live)
 	s->mode = (live && (fwd ? s->i < nk : s->i >= 0)) ? DSB_ISL_GRID : DSB_ISL_DONE;
 }
 
+/* Batch shapes: a grid batch is GG positions of the stride-3 grid; the first run batch after a
+ * hit (RUN1) is its two back neighbours + GR1 - 2 positions after it (most runs are short: on
+ * the ONT fixture half of the seeds are <= 10 long); the later run batches are GR positions, and
+ * never more than the run can still read: the scan stops at the position that makes the seed 61
+ * long (len > 60), so a run at length ln reads at most 61 - ln. */
+template <int GR>
+DSB_HD int dsb_isl_rw(const dsb_isl_t *s) { return DSB_MIN(GR, 61 - s->ln); }
+
 /* the position lane gl of the strand's lanes probes in this batch (GG positions per grid
  * batch, GR per run batch); -1: none */
-template <int GG, int GR>
+template <int GG, int GR, int GR1 = GR>
 DSB_HD int dsb_isl_pos(const dsb_isl_t *s, int gl)
 {
 	int d = s->fwd ? 1 : -1, q;
 	switch (s->mode) {
 	case DSB_ISL_GRID: if (gl >= GG) return -1; q = s->i + 3 * d * gl; break;
-	case DSB_ISL_RUN1: if (gl >= GR) return -1; q = gl < 2 ? s->h - d * (gl + 1) : s->h + d * (gl - 1); break;
-	case DSB_ISL_RUN: if (gl >= GR) return -1; q = s->p + d * gl; break;
+	case DSB_ISL_RUN1: if (gl >= GR1) return -1; q = gl < 2 ? s->h - d * (gl + 1) : s->h + d * (gl - 1); break;
+	case DSB_ISL_RUN: if (gl >= dsb_isl_rw<GR>(s)) return -1; q = s->p + d * gl; break;
 	default: return -1;
 	}
 	return (q >= 0 && q < s->nk) ? q : -1;
 }
 
 /* the lowest and highest position the batch probes (lo > hi: none) */
-template <int GG, int GR>
+template <int GG, int GR, int GR1 = GR>
 DSB_HD void dsb_isl_span(const dsb_isl_t *s, int *lo, int *hi)
 {
-	int a = 0, b = -1;
+	int a = 0, b = -1, rw = dsb_isl_rw<GR>(s);
 	if (s->fwd) {
 		switch (s->mode) {
 		case DSB_ISL_GRID: a = s->i; b = s->i + 3 * DSB_MIN(GG - 1, (s->nk - 1 - s->i) / 3); break;
-		case DSB_ISL_RUN1: a = s->h - 2; b = DSB_MIN(s->h + GR - 2, s->nk - 1); break;
-		case DSB_ISL_RUN: a = s->p; b = DSB_MIN(s->p + GR - 1, s->nk - 1); break;
+		case DSB_ISL_RUN1: a = s->h - 2; b = DSB_MIN(s->h + GR1 - 2, s->nk - 1); break;
+		case DSB_ISL_RUN: a = s->p; b = DSB_MIN(s->p + rw - 1, s->nk - 1); break;
 		}
 	} else {
 		switch (s->mode) {
 		case DSB_ISL_GRID: b = s->i; a = s->i - 3 * DSB_MIN(GG - 1, s->i / 3); break;
-		case DSB_ISL_RUN1: b = s->h + 2; a = DSB_MAX(s->h - (GR - 2), 0); break;
-		case DSB_ISL_RUN: b = s->p; a = DSB_MAX(s->p - (GR - 1), 0); break;
+		case DSB_ISL_RUN1: b = s->h + 2; a = DSB_MAX(s->h - (GR1 - 2), 0); break;
+		case DSB_ISL_RUN: b = s->p; a = DSB_MAX(s->p - (rw - 1), 0); break;
 		}
 	}
 	*lo = a;
@@ -408,7 +416,7 @@ DSB_HD void dsb_isl_span(const dsb_isl_t *s, int *lo, int *hi)
 
 /* one batch: bit g of mb = exist bit of dsb_isl_pos(s, g).  Returns 1 when a seed closes
  * (*so, *sl = CLY_seed offset / len as search_exist_kmer_M2 stores them). */
-template <int GG, int GR>
+template <int GG, int GR, int GR1 = GR>
 DSB_HD int dsb_isl_step(dsb_isl_t *s, uint32_t mb, uint32_t *so, uint32_t *sl)
 {
 	int d = s->fwd ? 1 : -1;
@@ -427,7 +435,7 @@ DSB_HD int dsb_isl_step(dsb_isl_t *s, uint32_t mb, uint32_t *so, uint32_t *sl)
 	}
 	if (s->mode != DSB_ISL_RUN1 && s->mode != DSB_ISL_RUN)
 		return 0;
-	int g = 0, cur = s->p, stop = 0;
+	int g = 0, cur = s->p, stop = 0, gr = s->mode == DSB_ISL_RUN ? dsb_isl_rw<GR>(s) : GR1;
 	if (s->mode == DSB_ISL_RUN1) { /* for (j = 1; j < STEP_EK; ++j) behind the hit */
 		if (mb & 1) {
 			s->off -= d;
@@ -440,7 +448,7 @@ DSB_HD int dsb_isl_step(dsb_isl_t *s, uint32_t mb, uint32_t *so, uint32_t *sl)
 		g = 2;
 		cur = s->h + d;
 	}
-	for (; g < GR; g++, cur += d) { /* the run: i + j < l_kmer_v / j <= i, len > 60 ends it */
+	for (; g < gr; g++, cur += d) { /* the run: i + j < l_kmer_v / j <= i, len > 60 ends it */
 		if (s->fwd ? cur >= s->nk : cur < 0) { stop = 1; break; }
 		if (!((mb >> g) & 1)) { stop = 1; break; }
 		if (++s->ln > 60) { stop = 1; break; }
@@ -563,8 +571,10 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_spset_t *s) { return dsb_spset_inse
  * The same set as an open-addressing hash (one per lane of the wave-cooperative seeding):
  * membership == "inserted since the last reset or since the last wrap of the reference's
  * 500-entry array" (a wrap is `l == m -> l = 0`, i.e. the array forgets everything), so a
- * generation counter replaces clearing.  A slot is {node, gen64}: gen64 = the launch tag << 24 |
- * the lane's generation (24 bits: a lane starts far fewer generations in one launch).  Launch
+ * generation counter replaces clearing.  A slot is {node, gen64}: gen64 = the set's tag + the
+ * lane's generation (24 bits: a lane starts far fewer generations in one launch).  The tag is the
+ * generation base of the pool set the wave holds (DSB_HSET_POOL, below), or without the pool the
+ * launch tag << 24, as follows.  Launch
  * tags come from one 64-bit counter for the whole process (every context of every GPU) and never
  * repeat below 2^40, so slots written by earlier launches — of any context whose workspace bytes
  * these are — never compare equal and read as empty: the table is never cleared.  Within one
@@ -577,13 +587,35 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_spset_t *s) { return dsb_spset_inse
 #define DSB_HSET_SLOTS (1u << DSB_HSET_LOG2) /* > 500: the reference's set never holds more */
 #define DSB_HSET_SLOT_U64 2
 #define DSB_HSET_GEN_BITS 24
+/* the tables of one 64-lane wave: 512 KB (64, not DSB_WV: host code sizes the pool and the
+ * workspaces, and DSB_WV is 1 outside the device pass) */
+#define DSB_HSET_WAVE_U64 ((uint64_t)DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS * 64)
+/* DSB_HSET_POOL (the GPU build): the tables live in a per-GPU pool of wave-sized sets that a
+ * seeding wave holds only while it seeds (dsb_hpool_acquire, dsb_kern.h), not in every read's
+ * workspace — 512 KB less per read, i.e. more reads per chunk.  A pool set carries its own
+ * generation base, advanced past every generation a holder used, so its slots are never cleared
+ * either.  The CPU emulator (tests/emu) mirrors one pool set, used by every read in turn. */
+#ifndef DSB_HSET_POOL
+#if defined(__HIPCC__)
+#define DSB_HSET_POOL 1
+#else
+#define DSB_HSET_POOL 0
+#endif
+#endif
 typedef struct { uint64_t *tab; uint32_t stride, gen; int l, m; uint64_t tag; } dsb_hset_t;
-/* slot tag: the launch's tag (a host counter bumped for every phase launch, so two launches —
- * FAST0/FAST1, SLOW0/SLOW1, later chunks reusing the same workspace bytes, overflow re-runs —
- * never share one) in the high word, the lane's generation in the low word */
+/* slot tag without the pool: the launch's tag (a host counter bumped for every phase launch, so
+ * two launches — FAST0/FAST1, SLOW0/SLOW1, later chunks reusing the same workspace bytes, overflow
+ * re-runs — never share one) in the high word, the lane's generation in the low word */
 DSB_HD uint64_t dsb_hset_tag(const dsb_read_ws *w)
 {
 	return w->launch_tag << DSB_HSET_GEN_BITS;
+}
+/* the set of this lane: `hset` holds the wave's DSB_WV interleaved tables; slot tags are `tag` +
+ * the lane's generation (generation 0 is never used: every seed resets the set first) */
+DSB_HD dsb_hset_t dsb_hset_make(uint64_t *hset, uint64_t tag)
+{
+	dsb_hset_t hs = {hset + DSB_HSET_SLOT_U64 * dsb_lane(), DSB_HSET_SLOT_U64 * DSB_WV, 0, 0, 500, tag};
+	return hs;
 }
 DSB_HD void dsb_set_reset(dsb_hset_t *s)
 {
@@ -600,7 +632,7 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_hset_t *s)
 		s->gen++;
 	}
 	uint32_t h = (uint32_t)((node * 0x9E3779B97F4A7C15ull) >> (64 - DSB_HSET_LOG2));
-	uint64_t g = s->tag | (s->gen & ((1u << DSB_HSET_GEN_BITS) - 1));
+	uint64_t g = s->tag + (s->gen & ((1u << DSB_HSET_GEN_BITS) - 1));
 	for (;;) {
 		uint64_t *slot = s->tab + (uint64_t)h * s->stride;
 		uint64_t sn = slot[0], sg = slot[1];
@@ -1336,14 +1368,13 @@ DSB_HDN void dsb_slow_classify(dsb_read_ws *w, const dsb_sdir_t *sd)
 }
 
 template <bool SLOW>
-DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, dsb_mem_t *memtmp, int32_t *lds)
+DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp, dsb_mem_t *memtmp, int32_t *lds)
 {
 	const dsb_dindex_t *ix = w->ix;
 	uint32_t lane = dsb_lane();
 	uint32_t n_sv = s_d->l_seed_v_f;
 	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV; /* dbg 32: tiny staging (tests the replay) */
-	dsb_hset_t hs = {hset + DSB_HSET_SLOT_U64 * lane, DSB_HSET_SLOT_U64 * DSB_WV, 0, 0, 500,
-			 dsb_hset_tag(w)};
+	dsb_hset_t &hs = *hsp; /* the caller reads the generations used back (the pool's base) */
 	uint8_t l_ek = (uint8_t)ix->l_ek;
 	int min_index = DSB_MIN_MEM_LEN_FAST - l_ek;
 	/* bwt_MEM_search parameters: fast src/cly.c:1500-1501, slow src/cly.c:1568-1570 */
@@ -1353,7 +1384,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 	int n_top = 0, total = 0;
 	uint8_t *bin_read = w->bin + (s_d->strand ? w->L : 0);
 	/* ---- top seeds, in order (tix) */
-	/* the read-hash region is free while seeding (>= 16 L bytes; n_sv <= L/3 + 1): 5 words per seed
+	/* the read-hash region is free while seeding (>= 8 L + 8 KB bytes; n_sv <= L/3 + 1): 5 words per seed
 	 * — 2 record words, the pass-1 list, the top-seed list and the pass-0 hand-out order */
 	uint32_t *rec = w->hh[0], *klist = rec + 2 * (uint64_t)n_sv, *tix = rec + 3 * (uint64_t)n_sv;
 	uint32_t *hand = rec + 4 * (uint64_t)n_sv; /* pass-0 hand-out order (DSB_SM_LPT) */
@@ -1913,14 +1944,21 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, 
 }
 
 /* fast_classify / slow_classify with one wavefront per read: the per-lane state machine */
-/* lds: 2 x DSB_WV int32 of workgroup-local memory */
-DSB_HDN void dsb_fast_classify_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, int32_t *lds)
+/* lds: 2 x DSB_WV int32 of workgroup-local memory; hset: the wave's sp_set tables, slot tags from
+ * `tag` on (dsb_hset_make).  Returns the lane's last generation: the wave's maximum + 1 is the
+ * next free tag offset of these tables. */
+DSB_HDN uint32_t dsb_fast_classify_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, uint64_t tag, int32_t *lds)
 {
-	dsb_seed_sm<false>(w, s_d, hset, w->mem, lds);
+	dsb_hset_t hs = dsb_hset_make(hset, tag);
+	dsb_seed_sm<false>(w, s_d, &hs, w->mem, lds);
+	return hs.gen;
 }
-DSB_HDN void dsb_slow_classify_sm(dsb_read_ws *w, const dsb_sdir_t *sd, uint64_t *hset, dsb_mem_t *memtmp, int32_t *lds)
+DSB_HDN uint32_t dsb_slow_classify_sm(dsb_read_ws *w, const dsb_sdir_t *sd, uint64_t *hset, uint64_t tag, dsb_mem_t *memtmp,
+				      int32_t *lds)
 {
-	dsb_seed_sm<true>(w, sd, hset, memtmp, lds);
+	dsb_hset_t hs = dsb_hset_make(hset, tag);
+	dsb_seed_sm<true>(w, sd, &hs, memtmp, lds);
+	return hs.gen;
 }
 
 /* ------------------------------------------------------------------ chaining */

@@ -21,6 +21,9 @@ extern "C" {
  * stats[DSB_N_STATS + 4 * (ph * DSB_TL_STRIDE + t)] (s_memrealtime, 100 MHz) */
 #define DSB_DBG_TIMELINE (1u << 12)
 #define DSB_TL_STRIDE (1u << 17)
+/* DSB_WAVE_DBG bit (tests): seeding waves hand their sp_set pool set back without moving its
+ * generation base on, so later holders meet slots that still match (dsb_hpool_release) */
+#define DSB_DBG_POOL_NOGEN (1u << 13)
 #define DSB_N_STATS 320 /* 32 counters x (9 phases of part A + k_classB) */
 #define DSB_STATS_B 288
 #define DSB_STATS_SEED 0 /* k_seed's Bloom-probe counters (ek1, ek2): the island phase's block (island itself probes nothing) */
@@ -91,6 +94,8 @@ int dsb_gpu_batch_stage(dsb_index *ix, int slot, const dsb_reads_t *reads, dsb_p
 void dsb_gpu_batch_recycle(dsb_index *ix, dsb_gpu_batch *b);
 int dsb_gpu_batch_device(const dsb_index *ix, const dsb_gpu_batch *b);
 int dsb_gpu_n_devices(const dsb_index *ix);
+/* before a streamed call: split each GPU's workspace HBM between its contexts (kernels.hip) */
+int dsb_gpu_fit_contexts(dsb_index *ix, char *err, size_t errn);
 int dsb_gpu_device_id(const dsb_index *ix, int slot);
 
 /* Number of visible devices (0 if HIP has none). */

@@ -188,6 +188,9 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 #ifndef DSB_ISL_GR
 #define DSB_ISL_GR 0 /* positions per run batch (0: DSB_ISLAND_G) */
 #endif
+#ifndef DSB_ISL_GR1
+#define DSB_ISL_GR1 0 /* positions of a run's first batch, 2 back neighbours included (0: as DSB_ISL_GR) */
+#endif
 
 template <int G, int STATS>
 __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
@@ -200,6 +203,7 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 	/* positions per grid / run batch (<= G lanes) */
 	constexpr int GG = DSB_ISL_GG > 0 && DSB_ISL_GG < G ? DSB_ISL_GG : G;
 	constexpr int GR = DSB_ISL_GR > 0 && DSB_ISL_GR < G ? DSB_ISL_GR : G;
+	constexpr int GR1 = DSB_ISL_GR1 >= 4 && DSB_ISL_GR1 < GR ? DSB_ISL_GR1 : GR;
 	(void)dbg; (void)ro; (void)n_overflow; (void)tag;
 	const uint32_t GM = G == 32 ? 0xffffffffu : ((1u << G) - 1);
 	uint32_t lane = threadIdx.x, sg = lane / G, gl = lane % G;
@@ -243,7 +247,7 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 		for (;;) {
 			if (!__ballot(s.mode != DSB_ISL_DONE))
 				break;
-			int q = dsb_isl_pos<GG, GR>(&s, (int)gl);
+			int q = dsb_isl_pos<GG, GR, GR1>(&s, (int)gl);
 			int b = 0;
 			uint32_t pv = 0;
 #if DSB_ISL_WIN
@@ -251,7 +255,7 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 			 * group holds word wb + gl of a G-word window, reloaded (one coalesced load) only
 			 * when the batch leaves it; each k-mer's four words come by lane shuffles */
 			int lo, hi;
-			dsb_isl_span<GG, GR>(&s, &lo, &hi);
+			dsb_isl_span<GG, GR, GR1>(&s, &lo, &hi);
 			int64_t klo = ((int64_t)lo + bo) >> 3, khi = (((int64_t)hi + bo) >> 3) + 3;
 			if (s.mode != DSB_ISL_DONE && lo <= hi && (klo < wb || khi >= wb + G)) {
 				wb = s.fwd ? klo : DSB_MAX(khi - (G - 1), wmin);
@@ -290,7 +294,7 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 			if (q >= 0 && (s.mode != DSB_ISL_GRID || (mb && (int)gl == __builtin_ctz(mb))))
 				pre[q] = pv;
 			uint32_t so = 0, sl = 0;
-			if (dsb_isl_step<GG, GR>(&s, mb, &so, &sl) && gl == 0) {
+			if (dsb_isl_step<GG, GR, GR1>(&s, mb, &so, &sl) && gl == 0) {
 				uint32_t m = top.n, ti;
 				seed_v[m].offset = so;
 				seed_v[m].len = sl;
@@ -493,6 +497,62 @@ __global__ __launch_bounds__(DSB_HL_WG, DSB_HASH_LDS_KL <= 13 ? 4 : 2) void k_ha
 	for (uint32_t k = tid; k <= KEY_MASK; k += DSB_HL_WG) g_heads[k] = heads[k];
 }
 
+/* The seeding sp_set pool (DSB_HSET_POOL): a wave takes a free set for its seeding call and hands
+ * it back with the set's generation base moved past every generation its lanes used.
+ *
+ * The pool is split by XCD (hpool_nx partitions of hpool_part sets), and a wave takes a set of its
+ * own XCD's partition: the sets' slots are written with ordinary stores, which an XCD's L2 holds
+ * back (write-back, not coherent with the other XCDs' L2s), so every holder of a set must sit
+ * behind the same L2.  That makes the hand-over cheap: no agent-scope acquire / release, whose
+ * fences write back and invalidate the whole L2 (buffer_wbl2 / buffer_inv sc1) — with them the
+ * fast seeding ran 11-15% slower (C2 proxy).  Lane 0 takes the set with a relaxed CAS on its owner
+ * flag (device-scope atomics are performed past the L2s), probing from slot `start`; a partition
+ * holds at least as many sets as its XCD holds waves, so a free set always exists and the probe
+ * ends.  On release the wave first waits for its own slot stores to reach the L2
+ * (s_waitcnt vmcnt(0)), then stores the new base, waits again, and clears the owner flag, so the
+ * next holder reads the new base and finds every slot of this holder in the L2.  A next holder
+ * may still see an older copy of a line in its CU's L1: older lines hold older generations,
+ * which never match. */
+#if DSB_HSET_POOL
+#if defined(__HIP_DEVICE_COMPILE__)
+static_assert(DSB_HSET_WAVE_U64 == (uint64_t)DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS * DSB_WV, "a pool set holds one wave's tables");
+#endif
+__device__ __forceinline__ uint32_t dsb_hpool_acquire(const dsb_dindex_t *ix, uint32_t start, uint64_t *gen_base)
+{
+	uint32_t s = 0, glo = 0, ghi = 0;
+	if (dsb_lane() == 0) {
+		uint32_t xcc = ((uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xfu) % ix->hpool_nx; /* HW_REG_XCC_ID */
+		uint32_t mask = ix->hpool_part - 1, base = xcc * ix->hpool_part, q = start & mask;
+		for (;;) {
+			uint32_t expect = 0;
+			if (__hip_atomic_compare_exchange_strong(ix->hpool_own + base + q, &expect, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+								 __HIP_MEMORY_SCOPE_AGENT))
+				break;
+			q = (q + 1) & mask;
+		}
+		s = base + q;
+		uint64_t g = __hip_atomic_load(ix->hpool_gen + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		glo = (uint32_t)g;
+		ghi = (uint32_t)(g >> 32);
+	}
+	*gen_base = ((uint64_t)(uint32_t)dsb_wshfl((int)ghi, 0) << 32) | (uint32_t)dsb_wshfl((int)glo, 0);
+	return (uint32_t)dsb_wshfl((int)s, 0);
+}
+/* the next holder's tags start past `last_gen`, the wave's highest generation */
+__device__ __forceinline__ void dsb_hpool_release(const dsb_dindex_t *ix, uint32_t s, uint64_t gen_base, uint32_t last_gen, uint32_t dbg)
+{
+	uint32_t top = (uint32_t)dsb_wmax((int)last_gen);
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); /* keeps the slot stores above the wait */
+	__builtin_amdgcn_s_waitcnt(0);                        /* every lane's slot stores are in the L2 */
+	if (dsb_lane() == 0) {
+		if (!(dbg & DSB_DBG_POOL_NOGEN)) /* tests: keep the base, so the next holder meets live slots */
+			__hip_atomic_store(ix->hpool_gen + s, gen_base + top + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		__builtin_amdgcn_s_waitcnt(0);
+		__hip_atomic_store(ix->hpool_own + s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+}
+#endif
+
 /* One read of a phase of part A with one wavefront per read (dsb_wave.h): fast seeding
  * (FAST0/FAST1), chaining (RESOLVE_*), scoring (DELA).  The last phase publishes the read's
  * summary like k_phase. */
@@ -525,18 +585,33 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 		w.tmr = tmr_lds;
 	int active = dsb_phase_active(&w, &f, ph);
 	if (active) {
-		if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
+		if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1 || ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) {
+			/* no clearing: slots carry the set's tag (dsb_set_insert) */
+#if DSB_HSET_POOL
+			uint64_t hs_tag;
+			/* tests (DSB_DBG_POOL_NOGEN): sets picked by read length, so a copy of a read meets
+			 * the set an earlier copy used */
+			uint32_t ps = dsb_hpool_acquire(ix, (dbg & DSB_DBG_POOL_NOGEN) ? (L * 0x9E3779B1u) >> 19 : t, &hs_tag);
+			uint64_t *hset = ix->hpool + (uint64_t)ps * DSB_HSET_WAVE_U64;
+#else
 			uint64_t *hset = (uint64_t *)(base + lay.hset);
-			/* no clearing: slots carry the launch tag (dsb_set_insert) */
-			__shared__ int32_t sm_lds[2 * 64];
-			__shared__ uint8_t hb_lds_f[DSB_HB_LDS];
-			w.lds_hb = hb_lds_f;
-			dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, sm_lds);
-		} else if (ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) {
-			uint64_t *hset = (uint64_t *)(base + lay.hset);
-			/* no clearing: slots carry the launch tag (dsb_set_insert) */
-			__shared__ int32_t sm_lds2[2 * 64];
-			dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem, sm_lds2);
+			uint64_t hs_tag = dsb_hset_tag(&w);
+#endif
+			uint32_t last_gen;
+			if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
+				__shared__ int32_t sm_lds[2 * 64];
+				__shared__ uint8_t hb_lds_f[DSB_HB_LDS];
+				w.lds_hb = hb_lds_f;
+				last_gen = dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, hs_tag, sm_lds);
+			} else {
+				__shared__ int32_t sm_lds2[2 * 64];
+				last_gen = dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, hs_tag, w.mem, sm_lds2);
+			}
+#if DSB_HSET_POOL
+			dsb_hpool_release(ix, ps, hs_tag, last_gen, dbg);
+#else
+			(void)last_gen;
+#endif
 		} else if (ph == DSB_PH_RESOLVE_F || ph == DSB_PH_RESOLVE_S0 || ph == DSB_PH_RESOLVE_S1) {
 			__shared__ uint64_t sort_key[DSB_SORT_LDS];
 			__shared__ uint32_t sort_id[DSB_SORT_LDS];

@@ -19,7 +19,16 @@ static_assert(DSB_BIN_TAIL == DSB_BIN_TAIL_BYTES, "the scoring's read-range copy
 
 DSB_HD uint64_t dsb_al(uint64_t x) { return (x + 255) & ~255ull; }
 
-DSB_HD int dsb_key_len(uint32_t q_len) { return dsb_hash_kl(q_len); } /* the read hash's key bits */
+/* the read hash's key bits, which size its head tables: the GPU build's scoring looks the hash up
+ * as k_hash_lds built it, at most DSB_HASH_LDS_KL bits (dsb_build_hash_table); the CPU emulator and
+ * the lane-per-read phase kernels build it themselves at dsb_hash_kl bits */
+#ifndef DSB_WS_HASH_LDS
+#define DSB_WS_HASH_LDS DSB_HSET_POOL
+#endif
+DSB_HD int dsb_key_len(uint32_t q_len)
+{
+	return DSB_WS_HASH_LDS && dsb_hash_lds_read(q_len) ? dsb_hash_kl_lds(q_len) : dsb_hash_kl(q_len);
+}
 
 DSB_HD dsb_caps_t dsb_default_caps(uint32_t L, uint32_t scale)
 {
@@ -62,7 +71,7 @@ DSB_HD dsb_ws_layout dsb_layout(uint32_t L, dsb_caps_t cap)
 	o.win = p; p = dsb_al(p + DSB_WIN_BYTES);
 	o.mem = p; p = dsb_al(p + sizeof(dsb_mem_t) * 16 * 64); /* 16 MEM results per lane (slow seeding) */
 	o.spset = p; p = dsb_al(p + 8 * 512);
-	o.hset = p; p = dsb_al(p + 8ull * DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS * 64); /* per-lane sp_set hashes */
+	o.hset = p; p = dsb_al(p + (DSB_HSET_POOL ? 0 : 8ull * DSB_HSET_WAVE_U64)); /* per-lane sp_set hashes (else the pool) */
 	o.state = p; p = dsb_al(p + DSB_STATE_BYTES); /* dsb_rstate_t: state between phase launches */
 	o.total = p;
 	return o;

@@ -272,8 +272,6 @@ struct dsb_gpu_dev {
 	dbuf vlen, vso, vidx, vtid; /* the deferred overflow re-runs of a batch (batch_run) */
 	hipEvent_t evh[2][2];    /* k_hash_lds before the scoring launch, per stream (launch_phase) */
 	int evh_used[2] = {0, 0};
-	uint64_t tag = 0;        /* tag of this context's last phase launch (dsb_hset_tag; next_launch_tag) */
-	uint64_t tag_ctx = 0;    /* DSB_TEST_TAG_PER_CTX: round 3's per-context counter (tests only) */
 	/* streamed batches (read_classify pipeline): uploads on their own stream through pinned
 	 * staging, under their own lock, beside the kernels of the batch before */
 	hipStream_t cstream;
@@ -285,6 +283,7 @@ struct dsb_gpu_dev {
 	int pin_next = 0;
 	std::vector<dsb_gpu_batch *> spare; /* recycled batches: their device buffers are reused, never freed mid-pipeline */
 	int n_ctx = 1;           /* contexts on this GPU (they split its workspace budget) */
+	size_t pipe_budget = 0;  /* chunk workspace budget of a streamed batch (dsb_gpu_fit_contexts) */
 };
 
 template <typename T>
@@ -383,6 +382,33 @@ static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu
 		if (upload(g, ix->ref_tid, ix->n_ref + 1, &h.ref_tid, err, errn)) return -1;
 		if (upload(g, ix->p_tid, ix->max_tid + 1, &h.p_tid, err, errn)) return -1;
 		h.max_tid = ix->max_tid;
+	}
+	if (DSB_HSET_POOL) {
+		/* the seeding sp_set pool, shared by the contexts on this GPU: a partition per XCD, one
+		 * set per wave the XCD can hold (32 per CU), rounded up to a power of two; zero-filled, so
+		 * no slot matches a tag before its first writer (generation 0 is never used) */
+		hipDeviceProp_t prop;
+		HIP_OK(hipGetDeviceProperties(&prop, device));
+		int nx = 1;
+		if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, device) != hipSuccess || nx < 1)
+			nx = 1;
+		uint64_t per_cu = DSB_MAX(32u, (uint32_t)prop.maxThreadsPerMultiProcessor / 64u);
+		uint64_t waves = ((uint64_t)prop.multiProcessorCount + nx - 1) / nx * per_cu, part = 1;
+		while (part < waves)
+			part <<= 1;
+		uint64_t n = part * (uint64_t)nx;
+		void *p;
+		HIP_OK(hipMalloc(&p, 8 * DSB_HSET_WAVE_U64 * n));
+		HIP_OK(hipMemset(p, 0, 8 * DSB_HSET_WAVE_U64 * n));
+		g->allocs.push_back(p);
+		h.hpool = (uint64_t *)p;
+		HIP_OK(hipMalloc(&p, 12 * n));
+		HIP_OK(hipMemset(p, 0, 12 * n));
+		g->allocs.push_back(p);
+		h.hpool_gen = (uint64_t *)p;
+		h.hpool_own = (uint32_t *)((uint8_t *)p + 8 * n);
+		h.hpool_part = (uint32_t)part;
+		h.hpool_nx = (uint32_t)nx;
 	}
 	const dsb_dindex_t *dptr;
 	if (upload(g, &h, 1, &dptr, err, errn)) return -1;
@@ -576,9 +602,57 @@ static size_t ws_budget(const dsb_gpu_dev *g, int share)
 	 * number).  Fewer, larger chunks pay fewer phase-kernel tails and chunk turnarounds: on the C2
 	 * proxy (1M reads) a 192 GB budget (0.7 of free HBM) made 9 chunks, 250 GB 7 chunks:
 	 * 650.6k -> 694.4k reads/s (profiles/r04_k). */
+	if (share > 1 && g->pipe_budget)
+		return g->pipe_budget;
 	size_t b = (size_t)((double)(fr + g->ws.cap) * 0.88 / share);
 	size_t cap = (size_t)250 << 30;
 	return b < cap ? b : cap;
+}
+
+/* Before a streamed read_classify call: split the HBM the contexts of each GPU can use for chunk
+ * workspaces evenly between them.  A single-batch call may have grown one context's workspace to
+ * most of the GPU (ws_budget with share 1); left alone, the other contexts of that GPU would get
+ * chunks sized to what is left, and the streamed batches would run in many small chunks (C2 proxy,
+ * 100k reads: 326k -> 40k reads/s).  A workspace larger than its share is freed here, under its
+ * context's run lock (locks taken in context order, so concurrent calls cannot deadlock), and
+ * re-allocated at the share by the context's next batch. */
+extern "C" int dsb_gpu_fit_contexts(dsb_index *ix, char *err, size_t errn)
+{
+	if (getenv("DSB_WS_BUDGET_MB"))
+		return 0;
+	for (int k = 0; k < ix->n_gpu; k++) {
+		dsb_gpu_dev *g0 = (dsb_gpu_dev *)ix->gpus[k];
+		int first = 1;
+		for (int j = 0; j < k; j++)
+			first &= ((dsb_gpu_dev *)ix->gpus[j])->device != g0->device;
+		if (!first) /* this GPU was fitted with its first context */
+			continue;
+		std::vector<dsb_gpu_dev *> cs;
+		for (int j = k; j < ix->n_gpu; j++)
+			if (((dsb_gpu_dev *)ix->gpus[j])->device == g0->device)
+				cs.push_back((dsb_gpu_dev *)ix->gpus[j]);
+		for (dsb_gpu_dev *g : cs)
+			pthread_mutex_lock(&g->mu);
+		size_t fr = 0, tot = 0, held = 0;
+		int rc = hipSetDevice(g0->device) == hipSuccess && hipMemGetInfo(&fr, &tot) == hipSuccess ? 0 : -1;
+		for (dsb_gpu_dev *g : cs)
+			held += g->ws.cap;
+		/* the share, less dbuf::ensure's 1/8 growth margin; 250 GB at most (ws_budget) */
+		size_t per = (size_t)((double)(fr + held) * 0.88 / cs.size() / 1.13);
+		per = std::min(per, (size_t)250 << 30);
+		for (dsb_gpu_dev *g : cs) {
+			g->pipe_budget = rc ? 0 : per;
+			if (!rc && g->ws.cap > per + per / 8 + 8192) {
+				hipDeviceSynchronize(); /* the context's earlier launches may still read it */
+				g->ws.release();
+			}
+		}
+		for (size_t j = cs.size(); j-- > 0;)
+			pthread_mutex_unlock(&cs[j]->mu);
+	}
+	(void)err;
+	(void)errn;
+	return 0;
 }
 
 /* seed-wave prefix over a read list: 2 strands x ceil(lk/64) words for reads >= 40 bp */
@@ -619,32 +693,14 @@ static uint32_t wave_phases(void)
 	       (1u << DSB_PH_RESOLVE_S0) | (1u << DSB_PH_SLOW1) | (1u << DSB_PH_RESOLVE_S1) | (1u << DSB_PH_DELA);
 }
 
-/* Seeding sp_set slots carry the tag of the launch that wrote them (dsb_hset_tag) and are never
- * cleared, so a tag must never repeat on workspace bytes: one counter for the whole process
- * (every context of every GPU: a context's workspace may be re-allocated over bytes another
- * context wrote), and workspace buffers are zero-filled when allocated (tag 0 is never used). */
+/* Seeding sp_set slots are never cleared.  The GPU build keeps them in a per-GPU pool whose sets
+ * carry their own generation base (dsb_hpool_release); a DSB_HSET_POOL=0 build keeps them in each
+ * read's workspace, tagged with the launch that wrote them (dsb_hset_tag), so a tag must never
+ * repeat on workspace bytes: one counter for the whole process (every context of every GPU: a
+ * context's workspace may be re-allocated over bytes another context wrote), and workspace
+ * buffers are zero-filled when allocated (tag 0 is never used). */
 static std::atomic<uint64_t> g_launch_tag{0};
 static uint64_t next_launch_tag(void) { return ++g_launch_tag; }
-
-/* Test knobs for the tag-collision regression test (tests/test_gpu_parity.py): DSB_TEST_SHARED_WS=1
- * gives every context of the process one chunk workspace (runs serialised by a process-wide lock,
- * no zero fill between contexts: each context's launches meet the slots the others left), and
- * DSB_TEST_TAG_PER_CTX=1 brings back round 3's per-context tag counters, so that the test can show
- * it detects the collision the process-wide counter prevents. */
-static int test_env(const char *name)
-{
-	const char *e = getenv(name);
-	return e && atoi(e) != 0;
-}
-struct shared_ws_t {
-	pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
-	dbuf ws;
-};
-static shared_ws_t *shared_ws(void)
-{
-	static shared_ws_t *s = new shared_ws_t(); /* never freed: lives as long as the process */
-	return s;
-}
 
 /* the LDS read-hash build's time (ms_phase[DSB_PH_HASH]) since the last call, taken out of the
  * scoring phase's (the callers time the hash build + scoring launch pair together); the events
@@ -677,14 +733,12 @@ static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, 
 		abort();
 	}
 	uint32_t dbg = wave_dbg();
-	/* every launch gets its own slot tag; if the 32-bit counter ever wraps, the workspace is
-	 * cleared once (both streams drained) so that no slot of an earlier launch can match */
-	g->tag = test_env("DSB_TEST_TAG_PER_CTX") ? ++g->tag_ctx : next_launch_tag();
-	if (g->tag >= (1ull << (64 - DSB_HSET_GEN_BITS))) { /* 2^40 launches: unreachable in practice */
+	/* every launch gets its own slot tag (used by a DSB_HSET_POOL=0 build only) */
+	uint64_t tag = next_launch_tag();
+	if (!DSB_HSET_POOL && tag >= (1ull << (64 - DSB_HSET_GEN_BITS))) { /* 2^40 launches: unreachable in practice */
 		fprintf(stderr, "[dsb] launch tag space exhausted; reload the index\n");
 		abort();
 	}
-	uint64_t tag = g->tag;
 	if (ph == DSB_PH_DELA && DSB_HASH_LDS && m) {
 		/* the read hash in LDS (k_hash_lds), then the scoring; timed apart by hash_ms() */
 		int si = s == g->stream2;
@@ -960,15 +1014,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		     dsb_gpu_timing &T, char *err, size_t errn, const dsb_carry_hooks *hooks = nullptr)
 {
 	double hs[HS_N] = {0}, hs_t = now_ms();
-	/* DSB_TEST_SHARED_WS (tests): one chunk workspace for every context, runs serialised */
-	shared_ws_t *sw = test_env("DSB_TEST_SHARED_WS") ? shared_ws() : nullptr;
-	struct unlock_t {
-		shared_ws_t *sw;
-		~unlock_t() { if (sw) pthread_mutex_unlock(&sw->mu); }
-	} unlock_sw = {sw};
-	if (sw)
-		pthread_mutex_lock(&sw->mu);
-	dbuf &WS = sw ? sw->ws : g->ws;
+	dbuf &WS = g->ws;
 	auto hs_mark = [&](int k) {
 		double t = now_ms();
 		hs[k] += t - hs_t;

@@ -31,6 +31,9 @@ extern "C" dsb_phase_fn DSB_CAT(dsb_phase_kernel_, DSB_PH)(int wave, int stats)
 #else
 	if (wave)
 		return stats == 1 ? k_wave_phase<DSB_PH, 1> : (stats == 2 ? k_wave_phase<DSB_PH, 2> : k_wave_phase<DSB_PH, 0>);
+#if DSB_LANE_PHASES && DSB_WS_HASH_LDS
+#error "lane-per-read phases build the read hash at dsb_hash_kl bits: add -DDSB_WS_HASH_LDS=0"
+#endif
 #if DSB_LANE_PHASES
 	return stats == 1 ? k_phase<DSB_PH, 1> : (stats == 2 ? k_phase<DSB_PH, 2> : k_phase<DSB_PH, 0>);
 #else

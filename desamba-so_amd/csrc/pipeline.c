@@ -471,6 +471,8 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 		snprintf(err, errn, "index not resident on a GPU");
 		return -1;
 	}
+	if (dsb_gpu_fit_contexts(ix, err, errn))
+		return -1;
 	pipe_t P;
 	memset(&P, 0, sizeof(P));
 	pipe_t *p = &P;

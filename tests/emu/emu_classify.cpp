@@ -113,19 +113,18 @@ int main(int argc, char **argv)
 			}
 			if (getenv("EMU_WAVE")) { /* the wave-cooperative code paths, as a one-lane wave */
 				dsb_rflags_t f = {0, 0, 0, 0};
-				/* one sp_set table for all reads, never cleared, as the GPU reuses workspace bytes
-				 * across launches and chunks: only the per-launch slot tags keep it exact */
-				static std::vector<uint64_t> hset_store(DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS * 64, 0);
-				static uint32_t launch_tag = 0;
+				/* one sp_set table for all reads, never cleared, as a set of the GPU's pool
+				 * (dsb_kern.h dsb_hpool_release): only its moving generation base keeps it exact */
+				static std::vector<uint64_t> hset_store(DSB_HSET_WAVE_U64, 0);
+				static uint64_t gen_base = 0;
 				uint64_t *hset = hset_store.data();
 				for (int ph = 0; ph < DSB_PH_DELA; ph++) {
-					w.launch_tag = ++launch_tag;
 					if ((ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) && dsb_phase_active(&w, &f, ph)) {
 						static int32_t sm_lds[2];
-						dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, sm_lds);
+						gen_base += dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, gen_base, sm_lds) + 1;
 					} else if ((ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) && dsb_phase_active(&w, &f, ph)) {
 						static int32_t sm_lds2[2];
-						dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, w.mem, sm_lds2);
+						gen_base += dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, gen_base, w.mem, sm_lds2) + 1;
 					} else if (ph == DSB_PH_RESOLVE_F || ph == DSB_PH_RESOLVE_S0 || ph == DSB_PH_RESOLVE_S1) {
 						/* the resolve kernels' LDS sort / M3 staging arrays (garbage between reads) */
 						static uint64_t lds_key[DSB_SORT_LDS];

@@ -3,7 +3,7 @@
 // one-bit-at-a-time scan dsb_search_exist + the top-seed pass of dsb_seed_vector (the reference's
 // search_exist_kmer_M2 / get_seed_vector_M2, src/cly.c:1066-1229) over the same exist bits:
 // seeded random bit vectors of many densities, long runs (the len > 60 cut), lengths 0..3000,
-// both directions, grid / run batches of 4..32 positions.  The seed buffers start with the same
+// both directions, grid / run batches of 4..32 positions, first run batches of 4..8.  The seed buffers start with the same
 // garbage, so the stale top-byte writes must match too.  Exit status 0 iff everything agrees.
 #include <cstdio>
 #include <cstdlib>
@@ -40,7 +40,7 @@ static uint32_t ref_scan(const uint64_t *ex, uint32_t nk, dsb_seed_t *seed_v, ui
 }
 
 /* the batched form, lanes emulated: the stores k_island_g's group lane 0 makes */
-template <int GG, int GR>
+template <int GG, int GR, int GR1>
 static uint32_t batch_scan(const uint64_t *ex, uint32_t nk, dsb_seed_t *seed_v, uint32_t dir, uint32_t *total,
 			   uint64_t *probes)
 {
@@ -51,14 +51,14 @@ static uint32_t batch_scan(const uint64_t *ex, uint32_t nk, dsb_seed_t *seed_v, 
 	while (s.mode != DSB_ISL_DONE) {
 		uint32_t mb = 0;
 		for (int g = 0; g < 32; g++) {
-			int q = dsb_isl_pos<GG, GR>(&s, g);
+			int q = dsb_isl_pos<GG, GR, GR1>(&s, g);
 			if (q >= 0) {
 				(*probes)++;
 				if ((ex[q >> 6] >> (q & 63)) & 1) mb |= 1u << g;
 			}
 		}
 		uint32_t so = 0, sl = 0;
-		if (dsb_isl_step<GG, GR>(&s, mb, &so, &sl)) {
+		if (dsb_isl_step<GG, GR, GR1>(&s, mb, &so, &sl)) {
 			uint32_t m = top.n, ti;
 			seed_v[m].offset = so;
 			seed_v[m].len = sl;
@@ -72,7 +72,7 @@ static uint32_t batch_scan(const uint64_t *ex, uint32_t nk, dsb_seed_t *seed_v, 
 	return top.n;
 }
 
-template <int GG, int GR>
+template <int GG, int GR, int GR1 = GR>
 static long check(long trials, uint64_t *probes, uint64_t *positions)
 {
 	long bad = 0;
@@ -98,11 +98,11 @@ static long check(long trials, uint64_t *probes, uint64_t *positions)
 			b = a;
 			uint32_t ta = 0, tb = 0;
 			uint32_t la = ref_scan(ex.data(), nk, a.data(), dir, &ta);
-			uint32_t lb = batch_scan<GG, GR>(ex.data(), nk, b.data(), dir, &tb, probes);
+			uint32_t lb = batch_scan<GG, GR, GR1>(ex.data(), nk, b.data(), dir, &tb, probes);
 			*positions += nk;
 			if (la != lb || ta != tb || memcmp(a.data(), b.data(), cap * sizeof(dsb_seed_t))) {
 				if (bad < 5)
-					fprintf(stderr, "GG=%d GR=%d nk=%u dir=%u: seeds %u vs %u, total %u vs %u\n", GG, GR, nk, dir, la, lb, ta, tb);
+					fprintf(stderr, "GG=%d GR=%d GR1=%d nk=%u dir=%u: seeds %u vs %u, total %u vs %u\n", GG, GR, GR1, nk, dir, la, lb, ta, tb);
 				bad++;
 			}
 		}
@@ -114,7 +114,7 @@ int main(int argc, char **argv)
 {
 	st = argc > 1 ? strtoull(argv[1], 0, 10) | 1 : 1;
 	long n = argc > 2 ? atol(argv[2]) : 20000, bad = 0;
-	uint64_t pr[7] = {0}, pos[7] = {0};
+	uint64_t pr[10] = {0}, pos[10] = {0};
 	bad += check<4, 4>(n, &pr[0], &pos[0]);
 	bad += check<8, 8>(n, &pr[1], &pos[1]);
 	bad += check<16, 16>(n, &pr[2], &pos[2]);
@@ -122,8 +122,12 @@ int main(int argc, char **argv)
 	bad += check<16, 8>(n, &pr[4], &pos[4]);
 	bad += check<8, 16>(n, &pr[5], &pos[5]);
 	bad += check<12, 16>(n, &pr[6], &pos[6]);
-	printf("grid/run 4/4 8/8 16/16 32/32 16/8 8/16 12/16 probes per position:");
-	for (int k = 0; k < 7; k++) printf(" %.3f", (double)pr[k] / pos[k]);
-	printf("\nisl_check: %ld trials x 2 directions x 7 batch shapes, %ld mismatches\n", n, bad);
+	/* a narrower first run batch (RUN1: 2 back neighbours + GR1 - 2 after the hit) */
+	bad += check<8, 16, 8>(n, &pr[7], &pos[7]);
+	bad += check<8, 12, 4>(n, &pr[8], &pos[8]);
+	bad += check<4, 32, 6>(n, &pr[9], &pos[9]);
+	printf("grid/run/run1 4/4/4 8/8/8 16/16/16 32/32/32 16/8/8 8/16/16 12/16/16 8/16/8 8/12/4 4/32/6 probes per position:");
+	for (int k = 0; k < 10; k++) printf(" %.3f", (double)pr[k] / pos[k]);
+	printf("\nisl_check: %ld trials x 2 directions x 10 batch shapes, %ld mismatches\n", n, bad);
 	return bad != 0;
 }

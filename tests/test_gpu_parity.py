@@ -161,22 +161,23 @@ def test_concurrent_multi_batch_calls_share_contexts_without_deadlock(gpu_index)
     assert serial[0] == golden("mixed.herm.sam_full")
 
 
-def test_sp_set_tags_never_collide_across_contexts(pyd, fixture_index):
-    """Regression test for round 3's lost-anchor race: the seeding sp_set slots are never cleared
-    and match only the tag of the launch that wrote them, so a tag must never repeat on the same
-    workspace bytes, whichever context wrote them (kernels.hip next_launch_tag).  Deterministic
-    form: one chunk workspace for both contexts of DSB_DEVICES=0,0 (DSB_TEST_SHARED_WS), and the
-    same reads run first on one context and then again, at the same workspace offsets, on the other
-    (batch 0 = X on context 0, batch 1 = X X X X on context 1: DSB_PIPE_READS = 4 |X|, the first
-    batch being a quarter, DSB_TEST_ROUND_ROBIN for the batch-to-context order).  Every copy of X must give X's records.  With round 3's per-context
-    tag counters (DSB_TEST_TAG_PER_CTX) context 1's launches reuse context 0's tags over the same
-    sp_set slots and drop rows, which this test detects."""
+def test_sp_set_pool_sets_never_match_stale_slots(pyd, fixture_index):
+    """Regression test for round 3's lost-anchor race, in its round-4 form: the seeding sp_set
+    slots are never cleared; they live in a per-GPU pool of wave-sized sets that seeding waves take
+    and hand back (dsb_kern.h dsb_hpool_acquire / dsb_hpool_release), and a slot matches only the
+    generations of its current holder because every holder moves the set's generation base past the
+    generations it used.  Deterministic form: the same reads X run again and again (X X X X X over
+    two batches, DSB_PIPE_READS = 4 |X|, two contexts sharing one GPU's pool with
+    DSB_GPU_CONTEXTS=2, DSB_TEST_ROUND_ROBIN for the batch-to-context order), so the same reads'
+    seeding waves take sets that waves with the same nodes held before.  Every copy of X must give
+    X's records.  With the base kept in place and sets picked by read length (DSB_WAVE_DBG bit 13,
+    DSB_DBG_POOL_NOGEN), a later copy of a read takes the set an earlier copy filled, meets its
+    slots as live and drops anchors, which this test detects."""
     lines = golden("ont.fq").split(b"\n")
     x = b"\n".join(lines[:800]) + b"\n"  # the first 200 four-line records
     assert x.count(b"\n+\n") == 200
     data = x * 5
-    env = {"DSB_DEVICES": "0,0", "DSB_GPU_CONTEXTS": "1", "DSB_PIPE_READS": "800", "DSB_TEST_SHARED_WS": "1",
-           "DSB_TEST_ROUND_ROBIN": "1"}
+    env = {"DSB_DEVICES": "0", "DSB_GPU_CONTEXTS": "2", "DSB_PIPE_READS": "800", "DSB_TEST_ROUND_ROBIN": "1"}
 
     def run(extra):
         os.environ.update(env)
@@ -199,9 +200,10 @@ def test_sp_set_tags_never_collide_across_contexts(pyd, fixture_index):
     first = g[:200]
     for c in range(1, 5):
         assert g[200 * c:200 * (c + 1)] == first, f"copy {c} of the reads differs"
-    bad = run({"DSB_TEST_TAG_PER_CTX": "1"})
-    assert any(bad[200 * c:200 * (c + 1)] != bad[:200] for c in range(1, 5)), \
-        "per-context tags over shared workspace bytes should drop rows: the test would not detect the race"
+    assert first == groups(golden("ont.herm.sam"))[:200]
+    bad = run({"DSB_WAVE_DBG": str(1 << 13)})
+    assert bad != g, "pool sets handed back without moving their generation base should drop rows: " \
+        "the test would not detect stale slots"
 
 
 def test_two_calls_carry_pool_state_like_one_call(gpu_index, pyd):
