@@ -1367,13 +1367,16 @@ DSB_HDN void dsb_slow_classify(dsb_read_ws *w, const dsb_sdir_t *sd)
 	w->fast_classify = 0;
 }
 
-template <bool SLOW>
+template <bool SLOW, int G>
 DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp, dsb_mem_t *memtmp, int32_t *lds)
 {
 	const dsb_dindex_t *ix = w->ix;
-	uint32_t lane = dsb_lane();
+	/* G lanes per read (DSB_SM_G): the read's seeds run on a group of G lanes of the wave; `lane`
+	 * is the lane's index in its group, and every ballot, scan and broadcast is the group's */
+	constexpr uint32_t GW = (uint32_t)G < (uint32_t)DSB_WV ? (uint32_t)G : (uint32_t)DSB_WV;
+	uint32_t lane = dsb_glane<GW>();
 	uint32_t n_sv = s_d->l_seed_v_f;
-	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / DSB_WV; /* dbg 32: tiny staging (tests the replay) */
+	uint32_t S = (w->dbg & 32) ? 2 : w->cap.anc / GW; /* dbg 32: tiny staging (tests the replay) */
 	dsb_hset_t &hs = *hsp; /* the caller reads the generations used back (the pool's base) */
 	uint8_t l_ek = (uint8_t)ix->l_ek;
 	int min_index = DSB_MIN_MEM_LEN_FAST - l_ek;
@@ -1389,10 +1392,10 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 	uint32_t *rec = w->hh[0], *klist = rec + 2 * (uint64_t)n_sv, *tix = rec + 3 * (uint64_t)n_sv;
 	uint32_t *hand = rec + 4 * (uint64_t)n_sv; /* pass-0 hand-out order (DSB_SM_LPT) */
 	uint32_t m = 0;
-	for (uint32_t gb = 0; gb < n_sv; gb += DSB_WV) {
+	for (uint32_t gb = 0; gb < n_sv; gb += GW) {
 		uint32_t ci = gb + lane;
 		int t = ci < n_sv && (SLOW ? dsb_slow_takes(w, s_d, ci) : w->seeds[s_d->seed_off + ci].top != 0);
-		uint64_t bm = dsb_wballot(t);
+		uint64_t bm = dsb_gballot<GW>(t);
 		uint64_t below = (lane == 0) ? 0 : (bm & (~0ull >> (64 - lane)));
 		if (t)
 			tix[m + (uint32_t)__builtin_popcountll(below)] = ci;
@@ -1417,10 +1420,10 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 #pragma unroll
 #endif
 		for (int c = 0; c < DSB_SM_LPT_CH; c++)
-			slen[c] = seed_len((uint32_t)c * DSB_WV + lane);
+			slen[c] = seed_len((uint32_t)c * GW + lane);
 		uint32_t pos = 0;
 		auto place = [&](uint32_t q, int t) {
-			uint64_t bm = dsb_wballot(t);
+			uint64_t bm = dsb_gballot<GW>(t);
 			if (t) {
 				uint64_t below = lane == 0 ? 0 : (bm & (~0ull >> (64 - lane)));
 				hand[pos + (uint32_t)__builtin_popcountll(below)] = q;
@@ -1432,9 +1435,9 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 #pragma unroll
 #endif
 			for (int c = 0; c < DSB_SM_LPT_CH; c++)
-				if ((uint32_t)c * DSB_WV < m)
-					place((uint32_t)c * DSB_WV + lane, slen[c] == b);
-			for (uint32_t gb = DSB_SM_LPT_CH * DSB_WV; gb < m; gb += DSB_WV)
+				if ((uint32_t)c * GW < m)
+					place((uint32_t)c * GW + lane, slen[c] == b);
+			for (uint32_t gb = DSB_SM_LPT_CH * GW; gb < m; gb += GW)
 				place(gb + lane, seed_len(gb + lane) == b);
 		}
 		dsb_wsync();
@@ -1442,7 +1445,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 	dsb_anchor_t *anc0 = w->anc;
 	uint32_t n0 = w->n_anc, cap0 = w->cap.anc, of0 = w->overflow;
 	/* ---- per-lane seed state; every record starts as "overflowed" (replayed if never written) */
-	for (uint32_t q = lane; q < m; q += DSB_WV) {
+	for (uint32_t q = lane; q < m; q += GW) {
 		rec[2 * q] = 0;
 		rec[2 * q + 1] = 1u << 30;
 	}
@@ -1466,7 +1469,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 	w->n_anc = 0;
 	w->cap.anc = Sp;
 	w->overflow = 0;
-	uint32_t next_k = DSB_MIN((uint32_t)DSB_WV, mp); /* next seed of the pass to hand out (uniform) */
+	uint32_t next_k = DSB_MIN((uint32_t)GW, mp); /* next seed of the pass to hand out (uniform) */
 	uint32_t k = lane;                                 /* my top-seed index */
 	int st = DSB_SM_DONE;
 	uint32_t ci = 0, a_b = 0, seed_off = 0;
@@ -1526,14 +1529,14 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 		DSB_SM_START_SEED(lane);
 	uint64_t t_sm = DSB_T0();
 	for (;;) {
-		uint64_t act = dsb_wballot(st != DSB_SM_DONE);
+		uint64_t act = dsb_gballot<GW>(st != DSB_SM_DONE);
 		if (!act)
 			break;
 #ifdef DSB_EMU_PROF
 		prof_trips++;
 #endif
-		uint64_t mapm = dsb_wballot(st == DSB_SM_MAP);
-		int do_map = mapm != 0 && ((uint32_t)__builtin_popcountll(mapm) >= DSB_SM_MAP_BATCH || mapm == act);
+		uint64_t mapm = dsb_gballot<GW>(st == DSB_SM_MAP);
+		int do_map = mapm != 0 && ((uint32_t)__builtin_popcountll(mapm) >= DSB_MIN((uint32_t)DSB_SM_MAP_BATCH, GW) || mapm == act);
 		if (w->stats && lane == 0) { /* trip counters (stats kernels): trips, map trips, lanes mapping */
 			w->stats[DSB_ST_T_DPM]++;
 			if (do_map) {
@@ -1566,33 +1569,33 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 			cx.n_items = 0; /* timing experiment only */
 #endif
 			uint32_t cnt = inmap ? cx.n_items : 0;
-			uint32_t tot, pfx = dsb_wscan(cnt, &tot);
+			uint32_t tot, pfx = dsb_gscan<GW>(cnt, &tot);
 			uint32_t n_before = w->n_anc;
-			int32_t *own = lds, *omax = lds + DSB_WV; /* LDS: owner lane of each item of a chunk; kept max per owner */
+			int32_t *own = lds + 2 * dsb_gbase<GW>(), *omax = own + GW; /* LDS: owner lane of each item of a chunk; kept max per owner (the group's part) */
 			omax[lane] = 0;
-			for (uint32_t cb = 0; cb < tot; cb += DSB_WV) {
+			for (uint32_t cb = 0; cb < tot; cb += GW) {
 				uint32_t it = cb + lane;
 				if (inmap) /* owners label their items of this chunk */
-					for (uint32_t q = DSB_MAX(pfx, cb); q < pfx + cnt && q < cb + DSB_WV; q++)
+					for (uint32_t q = DSB_MAX(pfx, cb); q < pfx + cnt && q < cb + GW; q++)
 						own[q - cb] = (int32_t)lane;
 				dsb_wsync();
 				int o = it < tot ? own[lane] : 0;
 				dsb_wsync();
 				dsb_mapctx_t oc;
-				uint32_t opfx = (uint32_t)dsb_wshfl_any((int)pfx, o);
-				oc.rp_s = ((uint64_t)(uint32_t)dsb_wshfl_any((int)(uint32_t)(cx.rp_s >> 32), o) << 32) |
-					  (uint32_t)dsb_wshfl_any((int)(uint32_t)cx.rp_s, o);
-				oc.q_off = dsb_wshfl_any(cx.q_off, o);
-				oc.l_m = (uint32_t)dsb_wshfl_any((int)cx.l_m, o);
-				oc.u_off = (uint32_t)dsb_wshfl_any((int)cx.u_off, o);
+				uint32_t opfx = (uint32_t)dsb_gshfl_any<GW>((int)pfx, o);
+				oc.rp_s = ((uint64_t)(uint32_t)dsb_gshfl_any<GW>((int)(uint32_t)(cx.rp_s >> 32), o) << 32) |
+					  (uint32_t)dsb_gshfl_any<GW>((int)(uint32_t)cx.rp_s, o);
+				oc.q_off = dsb_gshfl_any<GW>(cx.q_off, o);
+				oc.l_m = (uint32_t)dsb_gshfl_any<GW>((int)cx.l_m, o);
+				oc.u_off = (uint32_t)dsb_gshfl_any<GW>((int)cx.u_off, o);
 				uint32_t pk1 = (uint32_t)cx.am_mtch | ((uint32_t)(uint16_t)cx.am_score << 16);
 				uint32_t pk2 = (uint32_t)cx.am_ll | ((uint32_t)cx.am_le << 8) | ((uint32_t)cx.am_rl << 16) |
 					       ((uint32_t)cx.am_re << 24);
 				uint32_t pk3 = (uint32_t)cx.ref_l | ((uint32_t)cx.ref_r << 1) | ((ci & 0xffffu) << 16);
-				pk1 = (uint32_t)dsb_wshfl_any((int)pk1, o);
-				pk2 = (uint32_t)dsb_wshfl_any((int)pk2, o);
-				pk3 = (uint32_t)dsb_wshfl_any((int)pk3, o);
-				uint32_t o_n = (uint32_t)dsb_wshfl_any((int)n_before, o);
+				pk1 = (uint32_t)dsb_gshfl_any<GW>((int)pk1, o);
+				pk2 = (uint32_t)dsb_gshfl_any<GW>((int)pk2, o);
+				pk3 = (uint32_t)dsb_gshfl_any<GW>((int)pk3, o);
+				uint32_t o_n = (uint32_t)dsb_gshfl_any<GW>((int)n_before, o);
 				oc.am_mtch = (uint16_t)pk1;
 				oc.am_score = (int16_t)(pk1 >> 16);
 				oc.am_ll = (uint8_t)pk2; oc.am_le = (uint8_t)(pk2 >> 8); oc.am_rl = (uint8_t)(pk2 >> 16);
@@ -1604,7 +1607,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 				uint64_t ti0 = DSB_T0();
 				int pass = it < tot ? dsb_map_item(w, &oc, it - opfx, &os, &an) : 0;
 				DSB_T1(DSB_ST_T_MATCH, ti0); /* lane 0: wave clocks in the REF_POS items themselves */
-				uint64_t pm = dsb_wballot(pass);
+				uint64_t pm = dsb_gballot<GW>(pass);
 				uint32_t start = opfx > cb ? opfx - cb : 0; /* the owner's first item in this chunk */
 				uint64_t before = (lane == 0 ? 0 : (~0ull >> (64 - lane))) & ~(start == 0 ? 0 : (~0ull >> (64 - start)));
 				uint32_t dest = o_n + (uint32_t)__builtin_popcountll(pm & before);
@@ -1616,7 +1619,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 					dsb_lds_max(omax + o, (int32_t)an.score);
 				/* owners: count their kept items of this chunk */
 				if (inmap) {
-					uint32_t lo = pfx > cb ? pfx - cb : 0, hi = DSB_MIN(pfx + cnt, cb + DSB_WV) - cb;
+					uint32_t lo = pfx > cb ? pfx - cb : 0, hi = DSB_MIN(pfx + cnt, cb + GW) - cb;
 					if (pfx + cnt > cb && lo < hi) {
 						uint64_t mine = (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & ~(lo == 0 ? 0ull : ((1ull << lo) - 1));
 						n_before += (uint32_t)__builtin_popcountll(pm & mine);
@@ -1792,7 +1795,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 					 (w->overflow ? 0u : (w->n_anc - a_b));
 		}
 		/* ---- hand the next top seeds to the lanes that finished one, in lane order */
-		uint64_t finm = dsb_wballot(st == DSB_SM_FIN);
+		uint64_t finm = dsb_gballot<GW>(st == DSB_SM_FIN);
 		if (finm) {
 			uint64_t below = (lane == 0) ? 0 : (finm & (~0ull >> (64 - lane)));
 			uint32_t mine = next_k + (uint32_t)__builtin_popcountll(below);
@@ -1836,10 +1839,10 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 #undef DSB_EMU_PROF_START
 	dsb_wsync();
 	if (pr == 0) { /* the seeds pass 1 runs again: records still flagged overflowed, in order */
-		for (uint32_t gb = 0; gb < m; gb += DSB_WV) {
+		for (uint32_t gb = 0; gb < m; gb += GW) {
 			uint32_t kk = gb + lane;
 			int o = kk < m && ((rec[2 * kk + 1] >> 30) & 1);
-			uint64_t bm = dsb_wballot(o);
+			uint64_t bm = dsb_gballot<GW>(o);
 			uint64_t below = (lane == 0) ? 0 : (bm & (~0ull >> (64 - lane)));
 			if (o)
 				klist[n_ovf + (uint32_t)__builtin_popcountll(below)] = kk;
@@ -1848,7 +1851,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 		dsb_wsync();
 		if (n_ovf && w->stats && lane == 0)
 			w->stats[DSB_ST_PASS2] += n_ovf;
-		S2 = (w->dbg & 32) ? 2 : cap0 / DSB_MIN((uint32_t)DSB_WV, DSB_MAX(n_ovf, 1u));
+		S2 = (w->dbg & 32) ? 2 : cap0 / DSB_MIN((uint32_t)GW, DSB_MAX(n_ovf, 1u));
 	}
 	} /* passes */
 	w->anc = anc0;
@@ -1858,22 +1861,22 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 	/* ---- skip rule + ordered compaction over the seed records */
 	int last_trig = 0;
 	uint32_t last_ci = 0;
-	for (uint32_t gb = 0; gb < m; gb += DSB_WV) {
+	for (uint32_t gb = 0; gb < m; gb += GW) {
 		uint32_t kk = gb + lane;
-		uint32_t gn = DSB_MIN((uint32_t)DSB_WV, m - gb);
+		uint32_t gn = DSB_MIN((uint32_t)GW, m - gb);
 		int act = kk < m;
 		uint32_t cix = act ? tix[kk] : 0;
 		uint32_t r0 = act ? rec[2 * kk] : 0, r1 = act ? rec[2 * kk + 1] : 0;
 		int trig = (int)(r1 >> 31), ovf = (int)((r1 >> 30) & 1);
 		uint32_t cnt = r1 & 0x3fffffffu, src_lane = (r0 >> 24) & 0x7fu, src_off = r0 & 0xffffffu, pool_ = r0 >> 31;
-		uint64_t tm = dsb_wballot(act && trig);
-		uint64_t om = dsb_wballot(act && ovf);
+		uint64_t tm = dsb_gballot<GW>(act && trig);
+		uint64_t om = dsb_gballot<GW>(act && ovf);
 		uint64_t skipm = 0;
 		int lt = last_trig;
 		uint32_t lc = last_ci;
 		int unknown = 0;
 		for (uint32_t q = 0; q < gn; q++) {
-			uint32_t cq = (uint32_t)dsb_wshfl((int)cix, (int)q);
+			uint32_t cq = (uint32_t)dsb_gshfl<GW>((int)cix, (int)q);
 			if (lt && cq == lc + 1) {
 				skipm |= 1ull << q;
 				lt = 0;
@@ -1889,7 +1892,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 			last_ci = lc;
 			if ((skipm >> lane) & 1)
 				cnt = 0;
-			uint32_t tot, off = dsb_wscan(cnt, &tot);
+			uint32_t tot, off = dsb_gscan<GW>(cnt, &tot);
 			if (w->n_anc + tot > w->cap.anc) {
 				w->overflow |= 1;
 				dsb_wsync();
@@ -1901,7 +1904,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 			w->n_anc += tot;
 		} else { /* seed by seed, in order, deciding the skips as the reference does */
 			for (uint32_t q = 0; q < gn; q++) {
-				uint32_t cq = (uint32_t)dsb_wshfl((int)cix, (int)q);
+				uint32_t cq = (uint32_t)dsb_gshfl<GW>((int)cix, (int)q);
 				if (last_trig && cq == last_ci + 1) {
 					last_trig = 0;
 					continue;
@@ -1920,16 +1923,16 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 					}
 				} else {
 					last_trig = (int)((tm >> q) & 1);
-					uint32_t kc = (uint32_t)dsb_wshfl((int)cnt, (int)q);
-					uint32_t sl = (uint32_t)dsb_wshfl((int)src_lane, (int)q), so = (uint32_t)dsb_wshfl((int)src_off, (int)q);
+					uint32_t kc = (uint32_t)dsb_gshfl<GW>((int)cnt, (int)q);
+					uint32_t sl = (uint32_t)dsb_gshfl<GW>((int)src_lane, (int)q), so = (uint32_t)dsb_gshfl<GW>((int)src_off, (int)q);
 					if (w->n_anc + kc > w->cap.anc) {
 						w->overflow |= 1;
 						dsb_wsync();
 						return;
 					}
-					uint32_t sp_ = (uint32_t)dsb_wshfl((int)pool_, (int)q);
+					uint32_t sp_ = (uint32_t)dsb_gshfl<GW>((int)pool_, (int)q);
 					const dsb_anchor_t *src = (sp_ ? w->anc_tmp2 + (uint64_t)sl * S2 : w->anc_tmp + (uint64_t)sl * S) + so;
-					for (uint32_t e = lane; e < kc; e += DSB_WV)
+					for (uint32_t e = lane; e < kc; e += GW)
 						w->anc[w->n_anc + e] = src[e];
 					w->n_anc += kc;
 				}
@@ -1947,17 +1950,19 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 /* lds: 2 x DSB_WV int32 of workgroup-local memory; hset: the wave's sp_set tables, slot tags from
  * `tag` on (dsb_hset_make).  Returns the lane's last generation: the wave's maximum + 1 is the
  * next free tag offset of these tables. */
+template <int G = 64>
 DSB_HDN uint32_t dsb_fast_classify_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, uint64_t tag, int32_t *lds)
 {
 	dsb_hset_t hs = dsb_hset_make(hset, tag);
-	dsb_seed_sm<false>(w, s_d, &hs, w->mem, lds);
+	dsb_seed_sm<false, G>(w, s_d, &hs, w->mem, lds);
 	return hs.gen;
 }
+template <int G = 64>
 DSB_HDN uint32_t dsb_slow_classify_sm(dsb_read_ws *w, const dsb_sdir_t *sd, uint64_t *hset, uint64_t tag, dsb_mem_t *memtmp,
 				      int32_t *lds)
 {
 	dsb_hset_t hs = dsb_hset_make(hset, tag);
-	dsb_seed_sm<true>(w, sd, &hs, memtmp, lds);
+	dsb_seed_sm<true, G>(w, sd, &hs, memtmp, lds);
 	return hs.gen;
 }
 

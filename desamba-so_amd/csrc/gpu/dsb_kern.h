@@ -553,19 +553,31 @@ __device__ __forceinline__ void dsb_hpool_release(const dsb_dindex_t *ix, uint32
 }
 #endif
 
-/* One read of a phase of part A with one wavefront per read (dsb_wave.h): fast seeding
- * (FAST0/FAST1), chaining (RESOLVE_*), scoring (DELA).  The last phase publishes the read's
- * summary like k_phase. */
+/* Lanes per read of the seeding phases (FAST0/1, SLOW0/1): 64 = a wave per read; 32 = two reads
+ * per wave, each on a half-wave group running the state machine of dsb_seed_sm on its own (a
+ * read's wave time is set by its longest seed, so the other lanes mostly wait: tools/seed_prof). */
+#ifndef DSB_SM_G
+#define DSB_SM_G 64
+#endif
+static_assert(DSB_SM_G == 64 || DSB_SM_G == 32, "lanes per read of the seeding phases: 64 or 32");
+#define DSB_PH_SEEDING(PH) ((PH) == DSB_PH_FAST0 || (PH) == DSB_PH_FAST1 || (PH) == DSB_PH_SLOW0 || (PH) == DSB_PH_SLOW1)
+#define DSB_PH_LANES(PH) (DSB_PH_SEEDING(PH) ? DSB_SM_G : 64)
+
+/* One read of a phase of part A with one wavefront per read (dsb_wave.h), or a group of
+ * DSB_PH_LANES(PH) lanes per read: fast seeding (FAST0/FAST1), chaining (RESOLVE_*), scoring
+ * (DELA).  `live`: the group has a read (the last wave of a launch may hold fewer).  The last
+ * phase publishes the read's summary like k_phase. */
 template <int PH, int STATS>
 __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 						const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
-						uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t t,
+						uint8_t *__restrict__ ws, const uint32_t *__restrict__ order, uint32_t t, int live,
 						dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow,
 						uint64_t *st, uint64_t *tmr_lds, unsigned long long *__restrict__ gstats,
 						uint32_t dbg, uint64_t tag)
 {
 	const int ph = PH;
-	uint32_t lane = threadIdx.x;
+	constexpr int G = DSB_PH_LANES(PH);
+	uint32_t lane = threadIdx.x & (G - 1); /* the lane's index in its read's group */
 	uint32_t r = order[t];
 	uint64_t tl0 = (DSB_TL && (dbg & DSB_DBG_TIMELINE)) ? __builtin_amdgcn_s_memrealtime() : 0;
 	uint32_t L = len[r];
@@ -583,33 +595,43 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 		w.stats = st;
 	if (STATS == 2)
 		w.tmr = tmr_lds;
-	int active = dsb_phase_active(&w, &f, ph);
-	if (active) {
-		if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1 || ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) {
-			/* no clearing: slots carry the set's tag (dsb_set_insert) */
+	int active = live && dsb_phase_active(&w, &f, ph);
 #if DSB_HSET_POOL
-			uint64_t hs_tag;
-			/* tests (DSB_DBG_POOL_NOGEN): sets picked by read length, so a copy of a read meets
-			 * the set an earlier copy used */
-			uint32_t ps = dsb_hpool_acquire(ix, (dbg & DSB_DBG_POOL_NOGEN) ? (L * 0x9E3779B1u) >> 19 : t, &hs_tag);
-			uint64_t *hset = ix->hpool + (uint64_t)ps * DSB_HSET_WAVE_U64;
-#else
+	/* the seeding wave's sp_set set: taken and handed back by the whole wave (its lanes' tables
+	 * serve the reads of all its groups), if any group seeds */
+	uint32_t ps = 0;
+	uint64_t hs_tag = 0;
+	uint64_t *hset = nullptr;
+	uint32_t last_gen = 0;
+	const int pool_wave = DSB_PH_SEEDING(PH) && __ballot(active) != 0;
+	if (pool_wave) {
+		/* tests (DSB_DBG_POOL_NOGEN): sets picked by the first group's read length, so a copy of
+		 * a read meets the set an earlier copy used */
+		uint32_t start = (dbg & DSB_DBG_POOL_NOGEN) ? ((uint32_t)__builtin_amdgcn_readfirstlane((int)L) * 0x9E3779B1u) >> 19
+							    : (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+		ps = dsb_hpool_acquire(ix, start, &hs_tag);
+		hset = ix->hpool + (uint64_t)ps * DSB_HSET_WAVE_U64;
+	}
+#endif
+	if (active) {
+		if (DSB_PH_SEEDING(PH)) {
+			/* no clearing: slots carry the set's tag (dsb_set_insert) */
+#if !DSB_HSET_POOL
 			uint64_t *hset = (uint64_t *)(base + lay.hset);
 			uint64_t hs_tag = dsb_hset_tag(&w);
-#endif
 			uint32_t last_gen;
+#endif
+			/* LDS: per group, 2 x G ints (dsb_seed_sm's owner / max arrays) */
 			if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
 				__shared__ int32_t sm_lds[2 * 64];
 				__shared__ uint8_t hb_lds_f[DSB_HB_LDS];
 				w.lds_hb = hb_lds_f;
-				last_gen = dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, hs_tag, sm_lds);
+				last_gen = dsb_fast_classify_sm<G>(&w, &w.sd[ph - DSB_PH_FAST0], hset, hs_tag, sm_lds);
 			} else {
 				__shared__ int32_t sm_lds2[2 * 64];
-				last_gen = dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, hs_tag, w.mem, sm_lds2);
+				last_gen = dsb_slow_classify_sm<G>(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, hs_tag, w.mem, sm_lds2);
 			}
-#if DSB_HSET_POOL
-			dsb_hpool_release(ix, ps, hs_tag, last_gen, dbg);
-#else
+#if !DSB_HSET_POOL
 			(void)last_gen;
 #endif
 		} else if (ph == DSB_PH_RESOLVE_F || ph == DSB_PH_RESOLVE_S0 || ph == DSB_PH_RESOLVE_S1) {
@@ -637,6 +659,10 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 		} else
 			dsb_phase<true>(&w, &f, ph);
 	}
+#if DSB_HSET_POOL
+	if (pool_wave)
+		dsb_hpool_release(ix, ps, hs_tag, last_gen, dbg);
+#endif
 	__syncthreads();
 	if (lane == 0) {
 		if (active)
@@ -655,7 +681,7 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 				atomicAdd(n_overflow, 1u);
 		}
 	}
-	if (DSB_TL && (dbg & DSB_DBG_TIMELINE) && lane == 0 && t < DSB_TL_STRIDE) {
+	if (DSB_TL && (dbg & DSB_DBG_TIMELINE) && lane == 0 && live && t < DSB_TL_STRIDE) {
 		unsigned long long *e = gstats + DSB_N_STATS + 4ull * (PH * DSB_TL_STRIDE + t);
 		e[0] = tl0;
 		e[1] = __builtin_amdgcn_s_memrealtime();
@@ -665,7 +691,8 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 	}
 }
 
-/* A phase of part A, one wave per workgroup: workgroup t runs read order[t]. */
+/* A phase of part A, one wave per workgroup: workgroup t runs read order[t] (the seeding phases:
+ * 64 / DSB_SM_G reads per workgroup). */
 template <int PH, int STATS>
 __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
 						    const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
@@ -684,10 +711,14 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 			tmr_lds[lane] = 0;
 		__syncthreads();
 	}
-	uint32_t t = blockIdx.x;
-	if (t >= n)
+	/* DSB_PH_LANES(PH) lanes per read: workgroup b runs reads order[b * 64 / G ...] */
+	constexpr int G = DSB_PH_LANES(PH);
+	uint32_t t = G == 64 ? blockIdx.x : blockIdx.x * (64 / G) + lane / G, t0 = blockIdx.x * (64 / G);
+	if (t0 >= n)
 		return;
-	wave_phase_read<PH, STATS>(ix, len, ws_off, scale, ws, order, t, ro, n_overflow, st, tmr_lds, gstats, dbg, tag);
+	int live = t < n;
+	wave_phase_read<PH, STATS>(ix, len, ws_off, scale, ws, order, live ? t : t0, live, ro, n_overflow, st, tmr_lds, gstats, dbg,
+				   tag);
 	if (STATS == 1)
 		for (int k = 0; k < DSB_ST_N; k++)
 			if (st[k])

@@ -752,8 +752,8 @@ static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, 
 		hipEventRecord(g->evh[si][1], s);
 		g->evh_used[si] = 1;
 	}
-	if (wave)
-		hipLaunchKernelGGL(fn, dim3(m), dim3(64), 0, s, g->d, cl,
+	if (wave) /* a wave per read, or 64 / DSB_SM_G reads per wave in the seeding phases */
+		hipLaunchKernelGGL(fn, dim3(((uint64_t)m * DSB_PH_LANES(ph) + 63) / 64), dim3(64), 0, s, g->d, cl,
 				   g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, order, m, g->ro.as<dsb_read_out_t>(),
 				   g->cnt.as<uint32_t>(), g->stats.as<unsigned long long>(), dbg, tag);
 	else
