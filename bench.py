@@ -344,11 +344,17 @@ def dropin_leg(idx, fq: bytes, n_reads: int, nb: int, batch_sam_full_sha: str | 
     # allocated on first use and kept with the index (a service's steady state)
     L.read_classify(idx.h, fq, len(fq), C.byref(out), C.byref(n), 6, 1)
     L.dsb_free(out)
-    t = time.perf_counter()
-    L.read_classify(idx.h, fq, len(fq), C.byref(out), C.byref(n), 7, 1)
-    secs = time.perf_counter() - t
-    text = C.string_at(out.value, n.value) if out.value else b""
-    L.dsb_free(out)
+    # three timed calls (fresh thread_ids, so each carries its own max_read_l from 0): a single
+    # 0.2-0.3 s call varies by +-10% from run to run; the median is reported, every time kept
+    times, text = [], b""
+    for k in range(3):
+        t = time.perf_counter()
+        L.read_classify(idx.h, fq, len(fq), C.byref(out), C.byref(n), 7 + k, 1)
+        times.append(time.perf_counter() - t)
+        if k == 0:
+            text = C.string_at(out.value, n.value) if out.value else b""
+        L.dsb_free(out)
+    secs = sorted(times)[1]
     same = None
     if batch_sam_full_sha is not None:
         same = hashlib.sha256(text).hexdigest() == batch_sam_full_sha
@@ -360,6 +366,7 @@ def dropin_leg(idx, fq: bytes, n_reads: int, nb: int, batch_sam_full_sha: str | 
                                            "ms_seed", "ms_h2d", "ms_d2h")}
     stages.update({k: int(tm[k]) for k in ("n_batches", "n_devices", "n_view_records", "n_copied_records")})
     return {"value": round(n_reads / secs, 1), "unit": "reads/s", "secs": round(secs, 4),
+            "secs_all": [round(x, 4) for x in times], "value_of": "median of 3 calls",
             "gbases_per_s": round(nb / secs / 1e9, 4), "reads": n_reads, "input_bytes": len(fq),
             "output_bytes": n.value, "identical_to_batch_records": same, "pipeline": stages,
             "host_threads": int(os.environ.get("DSB_HOST_THREADS", "0")) or None,
@@ -564,10 +571,12 @@ def main():
             with open(tf) as f:
                 tj = json.load(f)
             # rocprof names carry the stats template argument ("k_wave_phase<8, 0>"): compare without it
-            tk = re.sub(r"<(\d+)(?:, \d+)*>", r"<\1>", tj.get("kernel") or "")
-            if tj.get("workload") == workload and tj.get("reads") == a.reads and tk == KERNEL_OF[dom]:
-                traffic = tj.get("hbm_bytes_per_launch")
-                traffic_cal = tj.get("hbm_bytes_per_launch_calibrated")
+            if tj.get("workload") == workload and tj.get("reads") == a.reads:
+                for ent in tj.get("kernels") or [tj]:
+                    tk = re.sub(r"<(\d+)(?:, \d+)*>", r"<\1>", ent.get("kernel") or "")
+                    if tk == KERNEL_OF[dom]:
+                        traffic = ent.get("hbm_bytes_per_launch")
+                        traffic_cal = ent.get("hbm_bytes_per_launch_calibrated")
         roof = {"bound": "hbm", "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 6), "traffic": traffic,
                 "traffic_calibrated": traffic_cal, "kernel": KERNEL_OF[dom],

@@ -2,9 +2,11 @@
 """profiles/traffic.json from two rocprofv3 --pmc passes of tools/gpu_session.sh (FETCH_SIZE in one,
 WRITE_SIZE in the other; they cannot share a pass on gfx950) over the same bench.py workload:
 
-    python tools/traffic_json.py gpurun_out/TAG WORKLOAD READS KERNEL_PREFIX PROFILE_TAG
+    python tools/traffic_json.py gpurun_out/TAG WORKLOAD READS KERNEL_PREFIX[,PREFIX...] PROFILE_TAG
 
-Per launch of the kernel (KERNEL_PREFIX, e.g. "k_wave_phase<8"): FETCH_SIZE and WRITE_SIZE (KB)
+Per launch of each kernel (KERNEL_PREFIX, e.g. "k_wave_phase<8"; the bench's dominant kernel can be
+either of two whose step times are close, so several may be given: "kernels" lists them all, and the
+first one's figures also sit at the top level): FETCH_SIZE and WRITE_SIZE (KB)
 summed over its dispatches of >= 1000 workgroups (the chunk launches the bench's HIP events time;
 an overflow re-run of a few reads is a small launch) / the number of those dispatches; hbm_bytes_per_launch = 2 x FETCH + WRITE
 (MI355X_MICROARCH.md: gfx950's FETCH_SIZE counts half of a streaming read's bytes), and the
@@ -55,14 +57,18 @@ def main():
             fdir = cf.rsplit("/", 1)[0]
         if "WRITE_SIZE" in ctr:
             wdir = cf.rsplit("/", 1)[0]
-    kname, fetch_kb, nf = per_launch(fdir, "FETCH_SIZE", prefix)
-    _, write_kb, nw = per_launch(wdir, "WRITE_SIZE", prefix)
-    out = {"workload": workload, "reads": int(reads), "kernel": kname, "tag": tag, "launches": [nf, nw],
-           "fetch_size_kb_per_launch": round(fetch_kb, 1), "write_size_kb_per_launch": round(write_kb, 1),
-           "hbm_bytes_per_launch": int(1024 * (2 * fetch_kb + write_kb)),
-           "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of 128-B requests)",
-           "hbm_bytes_per_launch_calibrated": int(1024 * (fetch_kb + write_kb)),
-           "calibration": "FETCH_SIZE + WRITE_SIZE: the random-access reading of profiles/r03_calib/calib.json"}
+    ents = []
+    for pf in prefix.split(","):
+        kname, fetch_kb, nf = per_launch(fdir, "FETCH_SIZE", pf)
+        _, write_kb, nw = per_launch(wdir, "WRITE_SIZE", pf)
+        ents.append({"kernel": kname, "launches": [nf, nw],
+                     "fetch_size_kb_per_launch": round(fetch_kb, 1), "write_size_kb_per_launch": round(write_kb, 1),
+                     "hbm_bytes_per_launch": int(1024 * (2 * fetch_kb + write_kb)),
+                     "hbm_bytes_per_launch_calibrated": int(1024 * (fetch_kb + write_kb))})
+    out = dict({"workload": workload, "reads": int(reads), "tag": tag}, **ents[0])
+    out.update({"correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of 128-B requests)",
+                "calibration": "FETCH_SIZE + WRITE_SIZE: the random-access reading of profiles/r03_calib/calib.json",
+                "kernels": ents})
     print(json.dumps(out, indent=1))
 
 
