@@ -101,6 +101,7 @@ dsb_parser *dsb_parser_new(const char *buf, uint64_t len);
 void dsb_parser_set_fast(dsb_parser *p, int fast);
 uint64_t dsb_parser_next(dsb_parser *p, dsb_reads_t *out, uint64_t max_reads, uint64_t max_bases);
 void dsb_parser_stats(const dsb_parser *p, uint64_t *n_fast, uint64_t *n_slow);
+uint64_t dsb_parser_left(const dsb_parser *p); /* input bytes not yet read (estimate) */
 void dsb_parser_free(dsb_parser *p);
 /* One kseq_t over resident text (the evaluation tools): kseq_read's return value; the accessors
  * return its buffers (NULL if never set; stale content kept as the reference keeps it). */

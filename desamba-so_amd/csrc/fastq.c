@@ -365,6 +365,12 @@ uint64_t dsb_parser_next(dsb_parser *p, dsb_reads_t *out, uint64_t max_reads, ui
 	return out->n - n0;
 }
 
+/* input bytes not yet read (an estimate: the reader's window start) */
+uint64_t dsb_parser_left(const dsb_parser *p)
+{
+	return p->ks.len > p->ks.begin ? p->ks.len - p->ks.begin : 0;
+}
+
 void dsb_parser_stats(const dsb_parser *p, uint64_t *n_fast, uint64_t *n_slow)
 {
 	*n_fast = p->n_fast;

@@ -70,6 +70,7 @@ typedef struct {
 	/* parser thread */
 	dsb_parser *ps;
 	uint64_t max_reads, max_bases, depth;
+	uint64_t first_div, tail_div; /* batch sizing (parser_main) */
 } pipe_t;
 
 typedef struct {
@@ -414,9 +415,20 @@ static void *parser_main(void *arg)
 		pthread_mutex_unlock(&p->mu);
 		double tp = now_ms();
 		pbatch *b = calloc(1, sizeof(pbatch));
-		/* the first batch is a quarter size, so the GPU starts sooner */
-		uint64_t mr = seq == 0 ? (p->max_reads + 3) / 4 : p->max_reads;
-		uint64_t got = b ? dsb_parser_next(p->ps, &b->reads, mr, p->max_bases) : 0;
+		/* batch sizes: the first batch is 1/first_div of a full one, so the GPU starts sooner;
+		 * when what is left of the input makes at most 1.5 full batches, it is cut into a large
+		 * batch and a last one of 1/tail_div of it, so that little formatting follows the last
+		 * GPU batch (FASTQ text: ~2 bytes per base) */
+		uint64_t mr = p->max_reads, mb = p->max_bases;
+		if (seq == 0) {
+			mr = (mr + p->first_div - 1) / p->first_div;
+			mb = (mb + p->first_div - 1) / p->first_div;
+		} else if (p->tail_div > 1) {
+			uint64_t left = dsb_parser_left(p->ps) / 2;
+			if (left <= mb + mb / 2 && left > mb / p->tail_div)
+				mb = left - left / p->tail_div;
+		}
+		uint64_t got = b ? dsb_parser_next(p->ps, &b->reads, mr, mb) : 0;
 		double dt = now_ms() - tp;
 		pthread_mutex_lock(&p->mu);
 		p->ms_parse += dt;
@@ -488,6 +500,9 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 	p->round_robin = env_u64("DSB_TEST_ROUND_ROBIN", 0) != 0;
 	p->max_reads = env_u64("DSB_PIPE_READS", 100000); /* measured (C2 proxy, 100k reads): 25k / 50k / 100k -> 278k / 292k / 317k reads/s */
 	p->max_bases = env_u64("DSB_PIPE_MBP", 400) * 1000000ull;
+	p->first_div = env_u64("DSB_PIPE_FIRST", 4);
+	p->tail_div = env_u64("DSB_PIPE_TAIL", 0);
+	if (p->first_div == 0) p->first_div = 1;
 	p->depth = env_u64("DSB_PIPE_DEPTH", 2 + 2 * (uint64_t)n_dev);
 	if (p->max_reads == 0) p->max_reads = 1;
 	if (p->depth < 2) p->depth = 2;

@@ -5,7 +5,7 @@
 #   bench[:ARGS]      python bench.py ARGS (default: the driver's defaults, 5 steps)   -> bench.json
 #   ab:VARS:ARGS      bench.py --no-cpu --no-stats --no-dropin ARGS for the default library and
 #                     each variant (VARS comma-separated): desamba-so_amd/lib/var_VAR.so, or
-#                     env.KEY.VALUE = the default library with KEY=VALUE (DROPIN= keeps the
+#                     env.KEY.VALUE[+KEY.VALUE] = the default library with KEY=VALUE (DROPIN= keeps the
 #                     drop-in leg)                                                     -> ab_*.json
 #   parity:VAR        tests/test_gpu_parity.py + test_gpu_c1.py with lib/var_VAR.so     -> parity_VAR.log
 #   scale[:K]         tests/test_gpu_scale.py -k K (C2 proxy, e-kmer table sizes)       -> scale.log
@@ -40,7 +40,8 @@ for step in "$@"; do
 			# a variant is lib/var_V.so, or env.KEY.VALUE (the default library with KEY=VALUE)
 			envs=()
 			if [ "$v" = base ]; then unset DSB_LIB
-			elif [[ $v == env.* ]]; then unset DSB_LIB; kv=${v#env.}; envs=("${kv%%.*}=${kv#*.}")
+			elif [[ $v == env.* ]]; then unset DSB_LIB; envs=(); IFS=+ read -ra kvs <<< "${v#env.}"
+				for kv in "${kvs[@]}"; do envs+=("${kv%%.*}=${kv#*.}"); done
 			else export DSB_LIB=desamba-so_amd/lib/var_$v.so; fi
 			env "${envs[@]}" timeout -k 10 300 $PY bench.py --no-cpu --no-stats ${DROPIN---no-dropin} $args > "$O/${name}_$v.json" 2> "$O/${name}_$v.err" || { tail -20 "$O/${name}_$v.err"; exit 1; }
 			python3 -c "import json; d=json.load(open('$O/${name}_$v.json')); print('$v', d['value'], d['ms_per_step'], {k: round(x, 1) for k, x in d['phase_ms_classA'].items()}, 'dropin', (d.get('dropin') or {}).get('value'), (d.get('dropin') or {}).get('identical_to_batch_records'))" | tee -a "$O/$name.txt"
