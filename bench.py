@@ -61,6 +61,10 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 METRIC = "long reads classified/sec + Gbases/sec at 1/2/4/8 MI355X; bit-exact taxid match"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+# random 64-B line rate measured on this hardware (profiles/r03_calib/calib.json: dependent 4-B
+# gathers over a 1 GB table, 55.92 G loads/s, one 64-B line each): the ceiling of the classify
+# kernels' access pattern, which is random lines, not streams
+RANDOM_LINE_PEAK_GBS = 55.92 * 64
 # the phase kernels of classify part A (kernels.hip launch_phase)
 KERNEL_OF = {"island": "k_island_g<16>", "fast0": "k_wave_phase<1>", "fast1": "k_wave_phase<2>",
              "resolve_f": "k_wave_phase<3>", "slow0": "k_wave_phase<4>", "resolve_s0": "k_wave_phase<5>",
@@ -577,9 +581,17 @@ def main():
                     if tk == KERNEL_OF[dom]:
                         traffic = ent.get("hbm_bytes_per_launch")
                         traffic_cal = ent.get("hbm_bytes_per_launch_calibrated")
+        rand = None
+        if traffic_cal and d["avg_launch_ms"] > 0:
+            ra = traffic_cal / (d["avg_launch_ms"] / 1e3) / 1e9
+            rand = {"achieved": round(ra, 1), "peak": round(RANDOM_LINE_PEAK_GBS, 1), "unit": "GB/s",
+                    "frac": round(ra / RANDOM_LINE_PEAK_GBS, 4),
+                    "note": "PMC HBM bytes per launch (FETCH_SIZE + WRITE_SIZE, the random-access calibration) "
+                            "over the measured random 64-B line rate; the kernel's time is set by dependent "
+                            "random transactions, not by streamed bytes (DESIGN.md section 6)"}
         roof = {"bound": "hbm", "achieved": d["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 6), "traffic": traffic,
-                "traffic_calibrated": traffic_cal, "kernel": KERNEL_OF[dom],
+                "traffic_calibrated": traffic_cal, "random_access": rand, "kernel": KERNEL_OF[dom],
                 "phase": dom, "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
                 "launches_per_step": d["launches_per_step"], "avg_launch_ms": d["avg_launch_ms"], "phases": per_phase}
         stats = {"phases": ts["stats_phase"], "classB": ts["stats_B"]}
