@@ -778,6 +778,10 @@ struct dsb_gpu_batch {
 	/* per-chunk processing order (longest first), cached: it depends on the lengths only */
 	std::vector<uint64_t> ord_cb, ord_ce;
 	std::vector<std::vector<uint32_t>> ord;
+	/* each read's workspace bytes at capacity scale wsz_scale (dsb_layout), cached: the chunk
+	 * partition of a rerun batch sums them instead of laying every read out again (9 ms per 1M) */
+	std::vector<uint64_t> wsz;
+	uint32_t wsz_scale = 0;
 };
 
 static const std::vector<uint32_t> &chunk_order(dsb_gpu_batch *b, uint64_t cb, uint64_t ce)
@@ -807,6 +811,10 @@ static int batch_upload(dsb_gpu_dev *g, const dsb_reads_t *reads, dsb_gpu_batch 
 	hipStream_t s = g->stream;
 	uint64_t n = reads->n;
 	b->n = n;
+	b->wsz.clear(); /* new reads: the cached sizes and orders are stale */
+	b->ord.clear();
+	b->ord_cb.clear();
+	b->ord_ce.clear();
 	b->len.resize(n);
 	b->seq_off.resize(n);
 	uint64_t tot = 0;
@@ -1157,8 +1165,14 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	for (uint64_t cb = 0; cb < n;) {
 		/* ---- chunk [cb, ce) within the workspace budget, input order */
 		uint64_t ce = cb, ws_total = 0;
+		if (b->wsz_scale != scale0 || b->wsz.size() != n) {
+			b->wsz.resize(n);
+			for (uint64_t i = 0; i < n; i++)
+				b->wsz[i] = dsb_layout(len[i], dsb_default_caps(len[i], scale0)).total;
+			b->wsz_scale = scale0;
+		}
 		while (ce < n) {
-			uint64_t sz = dsb_layout(len[ce], dsb_default_caps(len[ce], scale[ce])).total;
+			uint64_t sz = scale[ce] == scale0 ? b->wsz[ce] : dsb_layout(len[ce], dsb_default_caps(len[ce], scale[ce])).total;
 			if (ce > cb && ws_total + sz > budget)
 				break;
 			ws_off[ce] = ws_total;
@@ -1623,6 +1637,7 @@ extern "C" int dsb_gpu_batch_stage(dsb_index *ix, int slot, const dsb_reads_t *r
 		b->ord.clear();
 		b->ord_cb.clear();
 		b->ord_ce.clear();
+		b->wsz.clear();
 		uint64_t n = reads->n, tot = 0;
 		b->n = n;
 		b->len.resize(n);
