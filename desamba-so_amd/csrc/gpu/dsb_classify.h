@@ -938,6 +938,9 @@ DSB_HD dsb_anchor_t *dsb_push_anchor(dsb_read_ws *w)
 #define DSB_LV_L 12
 #define DSB_MIN_S_1 12
 #define DSB_MIN_S_2 20
+#ifndef DSB_MAP_SUF_EARLY
+#define DSB_MAP_SUF_EARLY 0
+#endif
 /* map_seed, src/cly.c:701-934, in two parts: dsb_map_seed_pre (locate the hit, extend and
  * score its prefix / suffix: src/cly.c:701-884) leaves the REF_POS list of the hit's unitig in
  * a context; dsb_map_item scores one REF_POS entry of it into an Anchor (src/cly.c:886-931).
@@ -997,11 +1000,23 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 			} else
 				l_pre = s_l;
 		}
+		int ts_pre = 0; /* the suffix window is loaded already */
 		if (uni >= 0) {
 			if (dsb_gld(ix->uni + uni).length < DSB_MIN_UNI_L)
 				break;
 			l_pre = DSB_MIN(l_pre, u_off);
 			dsb_get_ref_r(w, TP, t_off - 1, l_pre, 0);
+#if DSB_MAP_SUF_EARLY
+			/* the suffix's first window depends on t_off and l_m only: its load goes out with
+			 * the prefix window's instead of after the prefix extension (one round trip less) */
+			{
+				uint32_t lms = DSB_MIN(dsb_gld(ix->uni + uni).length - u_off - l_m, s_i->read_L - (q_off + l_m + 1));
+				if (lms != 0) {
+					dsb_get_ref_r(w, TS, t_off + l_m, DSB_MIN(lms, (uint32_t)DSB_LV_L), 1);
+					ts_pre = 1;
+				}
+			}
+#endif
 		}
 		d_pre = dsb_lv_extd_r(TP, l_pre, QP, l_pre);
 		s = dsb_qmem(ix, l_m) + dsb_gld(Q_LV + (d_pre * DSB_LV_DIM + l_pre));
@@ -1027,7 +1042,8 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 			l_suf = DSB_MIN(l_max_suf, (uint32_t)DSB_LV_L);
 			q_suf = q_b + q_off_r;
 			uint64_t ql = dsb_ld8u(q_suf), qh = dsb_ld8u(q_suf + 8);
-			dsb_get_ref_r(w, TS, t_off + l_m, l_suf, 1);
+			if (!ts_pre)
+				dsb_get_ref_r(w, TS, t_off + l_m, l_suf, 1);
 			if ((TS.b & 0xff) == (ql & 0xff)) {
 				uint32_t mtc;
 				do {
