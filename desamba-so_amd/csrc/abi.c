@@ -18,6 +18,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <pthread.h>
 #include <sys/mman.h>
 #include "dsb_host.h"
@@ -186,13 +187,24 @@ void read_classify(void *idx, char *input, uint64_t input_n, char **output, uint
 		fatal("read_classify", "cannot decompress input");
 	}
 	int mrl = st->max_read_l;
-	if (classify_resident(ix, buf, len, DSB_OUT_SAM_FULL, &mrl, output, output_n, NULL))
+	struct timespec c0, c1, c2;
+	clock_gettime(CLOCK_MONOTONIC, &c0);
+	dsb_timing_t tm;
+	memset(&tm, 0, sizeof(tm));
+	if (classify_resident(ix, buf, len, DSB_OUT_SAM_FULL, &mrl, output, output_n, &tm))
 		fatal("read_classify", "GPU classify failed");
+	clock_gettime(CLOCK_MONOTONIC, &c1);
 	st->max_read_l = mrl;
 	if (unmap)
 		munmap(buf, unmap);
 	else if (owned)
 		free(buf);
+	clock_gettime(CLOCK_MONOTONIC, &c2);
+	if (getenv("DSB_HOST_TIMING")) /* dev: where a call's wall time goes beyond the pipeline's */
+		fprintf(stderr, "[dsb call] pipeline %.1f ms (parse %.1f, wait_gpu %.1f, format %.1f), classify_resident %.1f ms, after %.1f ms\n",
+			tm.ms_total, tm.ms_parse, tm.ms_wait_gpu, tm.ms_format,
+			(c1.tv_sec - c0.tv_sec) * 1e3 + (c1.tv_nsec - c0.tv_nsec) / 1e6,
+			(c2.tv_sec - c1.tv_sec) * 1e3 + (c2.tv_nsec - c1.tv_nsec) / 1e6);
 }
 
 void meta_analysis(void *idx, char *input, uint64_t input_n, char **output, uint64_t *output_n, int thread_id,

@@ -637,12 +637,22 @@ extern "C" int dsb_gpu_fit_contexts(dsb_index *ix, char *err, size_t errn)
 		int rc = hipSetDevice(g0->device) == hipSuccess && hipMemGetInfo(&fr, &tot) == hipSuccess ? 0 : -1;
 		for (dsb_gpu_dev *g : cs)
 			held += g->ws.cap;
-		/* the share, less dbuf::ensure's 1/8 growth margin; 250 GB at most (ws_budget) */
+		/* the share, less dbuf::ensure's 1/8 growth margin; 250 GB at most (ws_budget).  A share
+		 * within 10% of the one already set is kept: free HBM moves a little from call to call
+		 * (staging, result buffers), and a workspace freed for a slightly smaller share is
+		 * re-allocated by the next batch (hundreds of ms for ~100 GB) */
 		size_t per = (size_t)((double)(fr + held) * 0.88 / cs.size() / 1.13);
 		per = std::min(per, (size_t)250 << 30);
 		for (dsb_gpu_dev *g : cs) {
-			g->pipe_budget = rc ? 0 : per;
-			if (!rc && g->ws.cap > per + per / 8 + 8192) {
+			if (rc) {
+				g->pipe_budget = 0;
+				continue;
+			}
+			size_t old = g->pipe_budget;
+			if (!(old && old <= per + per / 10 && per <= old + old / 10))
+				g->pipe_budget = per;
+			size_t b = g->pipe_budget;
+			if (g->ws.cap > b + b / 4 + 8192) {
 				hipDeviceSynchronize(); /* the context's earlier launches may still read it */
 				g->ws.release();
 			}
@@ -1187,7 +1197,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		if (WS.ensure(ws_total + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
 		    g->word_off.ensure(8 * (size_t)cn + 16, err, errn))
 			return -1;
-		if (WS.p != ws_before) /* fresh bytes: no stale sp_set slot may carry a live tag */
+		if (!DSB_HSET_POOL && WS.p != ws_before) /* fresh bytes: no stale sp_set slot may carry a live tag */
 			HIP_OK(hipMemsetAsync(WS.p, 0, WS.cap, s));
 		HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
 		HIP_OK(hipMemcpyAsync(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
