@@ -188,6 +188,9 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 #ifndef DSB_ISL_GR
 #define DSB_ISL_GR 0 /* positions per run batch (0: DSB_ISLAND_G) */
 #endif
+#ifndef DSB_ISL_SPEC2
+#define DSB_ISL_SPEC2 0 /* probe both Bloom tables at once (the second speculatively) */
+#endif
 #ifndef DSB_ISL_GR1
 #define DSB_ISL_GR1 0 /* positions of a run's first batch, 2 back neighbours included (0: as DSB_ISL_GR) */
 #endif
@@ -283,11 +286,22 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 				if (km) {
 					uint64_t h1 = dsb_hash64_1(km) & ix->ek_mask;
 					p1++;
+#if DSB_ISL_SPEC2
+					/* both tables' bytes in one round trip: the second probe is speculative (the
+					 * reference reads table 1 only after a table-0 hit; the bit is the same) */
+					uint64_t h2 = dsb_hash64_2(km) & ix->ek_mask;
+					uint8_t e0 = dsb_gld(ix->ek0 + (h1 >> 3)), e1 = dsb_gld(ix->ek1 + (h2 >> 3));
+					if ((e0 >> (7 - (h1 & 0x7))) & 0x1) {
+						p2++;
+						b = (e1 >> (7 - (h2 & 0x7))) & 0x1;
+					}
+#else
 					if ((dsb_gld(ix->ek0 + (h1 >> 3)) >> (7 - (h1 & 0x7))) & 0x1) {
 						uint64_t h2 = dsb_hash64_2(km) & ix->ek_mask;
 						p2++;
 						b = (dsb_gld(ix->ek1 + (h2 >> 3)) >> (7 - (h2 & 0x7))) & 0x1;
 					}
+#endif
 				}
 			}
 			uint32_t mb = (uint32_t)(__ballot(b) >> (sg * G)) & GM;
