@@ -94,8 +94,9 @@ int dsb_gpu_batch_stage(dsb_index *ix, int slot, const dsb_reads_t *reads, dsb_p
 void dsb_gpu_batch_recycle(dsb_index *ix, dsb_gpu_batch *b);
 int dsb_gpu_batch_device(const dsb_index *ix, const dsb_gpu_batch *b);
 int dsb_gpu_n_devices(const dsb_index *ix);
-/* before a streamed call: split each GPU's workspace HBM between its contexts (kernels.hip) */
-int dsb_gpu_fit_contexts(dsb_index *ix, char *err, size_t errn);
+/* before a streamed call of batches of up to max_reads reads: split each GPU's workspace HBM
+ * between its contexts and size their buffers for such batches (kernels.hip) */
+int dsb_gpu_fit_contexts(dsb_index *ix, uint64_t max_reads, char *err, size_t errn);
 int dsb_gpu_device_id(const dsb_index *ix, int slot);
 
 /* Number of visible devices (0 if HIP has none). */

@@ -278,6 +278,8 @@ struct dsb_gpu_dev {
 	pthread_mutex_t umu;
 	void *pin[2] = {nullptr, nullptr};
 	size_t pin_cap[2] = {0, 0};
+	void *bounce = nullptr;   /* pinned bounce buffer of the waited copies (copy_wait), under the run lock */
+	size_t bounce_cap = 0;
 	hipEvent_t pin_ev[2];
 	int pin_used[2] = {0, 0};
 	int pin_next = 0;
@@ -516,6 +518,8 @@ static void dev_free(dsb_gpu_dev *g)
 			hipHostFree(g->pin[k]);
 		hipEventDestroy(g->pin_ev[k]);
 	}
+	if (g->bounce)
+		hipHostFree(g->bounce);
 	hipStreamDestroy(g->cstream);
 	pthread_mutex_destroy(&g->umu);
 	for (void *p : g->allocs)
@@ -614,9 +618,11 @@ static size_t ws_budget(const dsb_gpu_dev *g, int share)
  * most of the GPU (ws_budget with share 1); left alone, the other contexts of that GPU would get
  * chunks sized to what is left, and the streamed batches would run in many small chunks (C2 proxy,
  * 100k reads: 326k -> 40k reads/s).  A workspace larger than its share is freed here, under its
- * context's run lock (locks taken in context order, so concurrent calls cannot deadlock), and
- * re-allocated at the share by the context's next batch. */
-extern "C" int dsb_gpu_fit_contexts(dsb_index *ix, char *err, size_t errn)
+ * context's run lock (try-locks: a GPU with a call in flight is left as that call fitted it),
+ * and the other buffers a batch of max_reads reads needs are sized here (the workspace itself
+ * grows with the batches, by doubling: pre-sizing it to the share held ~90% of the HBM for every
+ * loaded index, also for small inputs). */
+extern "C" int dsb_gpu_fit_contexts(dsb_index *ix, uint64_t max_reads, char *err, size_t errn)
 {
 	if (getenv("DSB_WS_BUDGET_MB"))
 		return 0;
@@ -631,8 +637,18 @@ extern "C" int dsb_gpu_fit_contexts(dsb_index *ix, char *err, size_t errn)
 		for (int j = k; j < ix->n_gpu; j++)
 			if (((dsb_gpu_dev *)ix->gpus[j])->device == g0->device)
 				cs.push_back((dsb_gpu_dev *)ix->gpus[j]);
-		for (dsb_gpu_dev *g : cs)
-			pthread_mutex_lock(&g->mu);
+		/* try-locks only: a batch of another call in flight holds its context's run lock while it
+		 * waits for the carry of its call's batch before, which may need another context's lock;
+		 * blocking here on one lock while holding another could close that cycle.  A busy context
+		 * means a call is running on this GPU, and that call has fitted the contexts already. */
+		size_t got = 0;
+		while (got < cs.size() && pthread_mutex_trylock(&cs[got]->mu) == 0)
+			got++;
+		if (got < cs.size()) {
+			while (got-- > 0)
+				pthread_mutex_unlock(&cs[got]->mu);
+			continue;
+		}
 		size_t fr = 0, tot = 0, held = 0;
 		int rc = hipSetDevice(g0->device) == hipSuccess && hipMemGetInfo(&fr, &tot) == hipSuccess ? 0 : -1;
 		for (dsb_gpu_dev *g : cs)
@@ -656,6 +672,19 @@ extern "C" int dsb_gpu_fit_contexts(dsb_index *ix, char *err, size_t errn)
 				hipDeviceSynchronize(); /* the context's earlier launches may still read it */
 				g->ws.release();
 			}
+			/* the buffers a batch of up to max_reads reads needs, at their full size now: grown
+			 * batch by batch they were freed and re-allocated whenever a context met a larger batch
+			 * than before, and hipFree waits for the whole GPU (the other context's kernels) */
+			uint64_t n = max_reads;
+			char e2[256];
+			if (b && n &&
+			    (g->scale.ensure(4 * n + 4, e2, sizeof(e2)) ||
+			     g->ws_off.ensure(8 * n + 8, e2, sizeof(e2)) || g->ro.ensure(sizeof(dsb_read_out_t) * n + 64, e2, sizeof(e2)) ||
+			     g->mrl.ensure(4 * n + 4, e2, sizeof(e2)) || g->hit_off.ensure(4 * n + 4, e2, sizeof(e2)) ||
+			     g->order.ensure(4 * n + 4, e2, sizeof(e2)) || g->word_off.ensure(8 * n + 16, e2, sizeof(e2)) ||
+			     g->hits.ensure(sizeof(dsb_hit_out_t) * 16 * n + 4096, e2, sizeof(e2)) ||
+			     g->wsr.ensure((size_t)64 << 20, e2, sizeof(e2))))
+				(void)hipGetLastError(); /* not fatal: the batches allocate what they need themselves */
 		}
 		for (size_t j = cs.size(); j-- > 0;)
 			pthread_mutex_unlock(&cs[j]->mu);
@@ -925,6 +954,49 @@ static int split_slow(void)
 	return v;
 }
 
+/* A copy between the device and pageable host memory on the context's stream, waited for, through
+ * the context's pinned bounce buffer.  A pageable copy (hipMemcpy, or hipMemcpyAsync on the
+ * stream) waited for the other context's kernels on the GPU: 60-150 ms inside a 250-450 ms
+ * read_classify call (the first batch's results, measured with DSB_HOST_TIMING); a pinned copy is
+ * a DMA on this stream only.  Large copies go in bounce-sized pieces. */
+static hipError_t copy_wait_g(dsb_gpu_dev *g, void *dst, const void *src, size_t n, hipMemcpyKind k, hipStream_t s)
+{
+	if (n == 0)
+		return hipSuccess;
+	const size_t want = std::min(n, (size_t)256 << 20);
+	if (g->bounce_cap < want) {
+		if (g->bounce)
+			hipHostFree(g->bounce);
+		g->bounce = nullptr;
+		g->bounce_cap = 0;
+		size_t c = std::max(want, (size_t)16 << 20);
+		hipError_t e = hipHostMalloc(&g->bounce, c, hipHostMallocDefault);
+		if (e != hipSuccess)
+			return e;
+		g->bounce_cap = c;
+	}
+	for (size_t o = 0; o < n; o += g->bounce_cap) {
+		size_t m = std::min(g->bounce_cap, n - o);
+		hipError_t e;
+		if (k == hipMemcpyDeviceToHost) {
+			e = hipMemcpyAsync(g->bounce, (const uint8_t *)src + o, m, k, s);
+			if (e == hipSuccess)
+				e = hipStreamSynchronize(s);
+			if (e == hipSuccess)
+				memcpy((uint8_t *)dst + o, g->bounce, m);
+		} else {
+			memcpy(g->bounce, (const uint8_t *)src + o, m);
+			e = hipMemcpyAsync((uint8_t *)dst + o, g->bounce, m, k, s);
+			if (e == hipSuccess)
+				e = hipStreamSynchronize(s);
+		}
+		if (e != hipSuccess)
+			return e;
+	}
+	return hipSuccess;
+}
+#define copy_wait(dst, src, n, k, s) copy_wait_g(g, (dst), (src), (n), (k), (s))
+
 /* The slow phases touch ~2% of the reads and leave most of the GPU idle: after resolve_f the
  * reads are split, the scoring of the rest runs on a second stream while the slow phases and
  * then the slow reads' scoring run on the first.  Returns 1 when the rest of part A ran here,
@@ -942,8 +1014,7 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 					       g->cnt2.as<uint32_t>());
 	HIP_OK(hipGetLastError());
 	uint32_t c2[2] = {0, 0};
-	HIP_OK(hipMemcpyAsync(c2, g->cnt2.p, 8, hipMemcpyDeviceToHost, s));
-	HIP_OK(hipStreamSynchronize(s));
+	HIP_OK(copy_wait(c2, g->cnt2.p, 8, hipMemcpyDeviceToHost, s));
 	if (c2[0] + c2[1] != cn) {
 		snprintf(err, errn, "split: %u + %u reads for a chunk of %u", c2[0], c2[1], cn);
 		return -1;
@@ -1027,6 +1098,7 @@ static int launch_classB(dsb_gpu_dev *g, dsb_gpu_batch *b, const uint32_t *cl, u
 							  g->stats.as<unsigned long long>());
 	return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
 
 static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_read_l, int stats_on,
 		     dsb_gpu_timing &T, char *err, size_t errn, const dsb_carry_hooks *hooks = nullptr)
@@ -1123,7 +1195,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				void *np = nullptr;
 				size_t need = rused + tot2 + (rused + tot2) / 2 + 4096;
 				HIP_OK(hipMalloc(&np, need));
-				HIP_OK(hipMemsetAsync(np, 0, need, s));
+				if (!DSB_HSET_POOL) /* launch-tagged sp_set tables: no stale tag in fresh bytes */
+					HIP_OK(hipMemsetAsync(np, 0, need, s));
 				if (rused)
 					HIP_OK(hipMemcpyAsync(np, g->wsr.p, rused, hipMemcpyDeviceToDevice, s));
 				HIP_OK(hipStreamSynchronize(s));
@@ -1142,14 +1215,14 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 					vws_off[cb + i] += rbase;
 				rused += tot2;
 			}
-			HIP_OK(hipMemcpyAsync(g->ws_off.p, vws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
-			HIP_OK(hipMemcpyAsync(g->scale.p, vscale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait(g->ws_off.p, vws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait(g->scale.p, vscale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
 			std::vector<uint64_t> wo2;
 			uint64_t tw2 = seed_words(vlen, cb, sel.data(), sel.size(), l_ek, wo2, nullptr);
 			if (g->sel.ensure(4 * sel.size() + 4, err, errn) || g->wo2.ensure(8 * wo2.size() + 16, err, errn))
 				return -1;
-			HIP_OK(hipMemcpyAsync(g->sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, s));
-			HIP_OK(hipMemcpyAsync(g->wo2.p, wo2.data(), 8 * wo2.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait(g->sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait(g->wo2.p, wo2.data(), 8 * wo2.size(), hipMemcpyHostToDevice, s));
 			uint32_t m = (uint32_t)sel.size();
 			if (m == 0) {
 				snprintf(err, errn, "overflow reported by the phase kernels but no read carries the flag");
@@ -1166,8 +1239,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			/* the re-run went to the non-blocking stream: drain it before the (null-stream) copies */
 			HIP_OK(hipStreamSynchronize(s));
 			hash_ms(g, 1); /* re-runs are not timed */
-			HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
-			HIP_OK(hipMemcpy(vro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
+			HIP_OK(copy_wait(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
+			HIP_OK(copy_wait(vro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
 		}
 		return 0;
 	};
@@ -1194,18 +1267,23 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		hs_mark(HS_SIZE);
 		uint64_t rused = 0; /* bytes of the retry buffer holding this chunk's re-run reads */
 		void *ws_before = WS.p;
-		if (WS.ensure(ws_total + 4096, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
+		/* a streamed batch's workspace grows by doubling (up to the context's share): each growth
+		 * is a hipFree, which waits for the whole GPU, the other context's kernels included */
+		size_t ws_want = ws_total + 4096;
+		if (hooks && ws_want > WS.cap)
+			ws_want = std::max(ws_want, std::min((size_t)budget, 2 * WS.cap));
+		if (WS.ensure(ws_want, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
 		    g->word_off.ensure(8 * (size_t)cn + 16, err, errn))
 			return -1;
 		if (!DSB_HSET_POOL && WS.p != ws_before) /* fresh bytes: no stale sp_set slot may carry a live tag */
 			HIP_OK(hipMemsetAsync(WS.p, 0, WS.cap, s));
-		HIP_OK(hipMemcpyAsync(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
-		HIP_OK(hipMemcpyAsync(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
 		const uint32_t *cl = b->d_len.as<uint32_t>() + cb;
 		const uint64_t *cso = b->d_seq_off.as<uint64_t>() + cb;
 		/* length-sorted order (longest first) for the one-lane-per-read kernels */
 		const std::vector<uint32_t> &order = chunk_order(b, cb, ce);
-		HIP_OK(hipMemcpyAsync(g->order.p, order.data(), 4ull * cn, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait(g->order.p, order.data(), 4ull * cn, hipMemcpyHostToDevice, s));
 		uint8_t *wsb = WS.as<uint8_t>();
 		hs_mark(HS_SETUP);
 		hipEventRecord(g->ev_a, s);
@@ -1223,8 +1301,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			uint64_t twB = seed_words(len, cb, order.data() + h, cn - h, l_ek, woB, &T.seed_positions);
 			if (g->woA.ensure(8 * woA.size() + 16, err, errn) || g->woB.ensure(8 * woB.size() + 16, err, errn))
 				return -1;
-			HIP_OK(hipMemcpyAsync(g->woA.p, woA.data(), 8 * woA.size(), hipMemcpyHostToDevice, s));
-			HIP_OK(hipMemcpyAsync(g->woB.p, woB.data(), 8 * woB.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait(g->woA.p, woA.data(), 8 * woA.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait(g->woB.p, woB.data(), 8 * woB.size(), hipMemcpyHostToDevice, s));
 			const uint32_t *oA = g->order.as<uint32_t>(), *oB = oA + h;
 			if (pipe_halves()) {
 				/* half A (longest reads) on the library stream, half B on the low-priority second
@@ -1307,7 +1385,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			}
 		} else {
 			tw = seed_words(len, cb, nullptr, cn, l_ek, word_off, &T.seed_positions);
-			HIP_OK(hipMemcpyAsync(g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait(g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
 			T.n_launch_phase += 1;
 		}
 		if (tw && DSB_ISLAND_G == 0) {
@@ -1345,8 +1423,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		hs_mark(HS_PARTA);
 		HIP_OK(hipStreamSynchronize(s));
 		uint32_t n_over = 0;
-		HIP_OK(hipMemcpy(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost));
-		HIP_OK(hipMemcpy(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
+		HIP_OK(copy_wait(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
 		hs_mark(HS_SYNC_A);
 		/* ---- max_read_l carry (src/cly.c:2953): prefix max over reads reaching the update; a
 		 * streamed batch takes its carry-in from the batch before it (possibly on another GPU)
@@ -1407,7 +1485,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		}
 		if (ce == n && hooks && hooks->carry_out)
 			hooks->carry_out(hooks->ctx, carry);
-		HIP_OK(hipMemcpyAsync(g->mrl.p, mrl.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait(g->mrl.p, mrl.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
 		if (g->hits.ensure(sizeof(dsb_hit_out_t) * worst + 4096, err, errn))
 			return -1;
 		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
@@ -1419,7 +1497,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				if (!h_ro[cb + i].status)
 					ordB.push_back(i);
 			cnB = (uint32_t)ordB.size();
-			HIP_OK(hipMemcpy(g->order.p, ordB.data(), 4ull * cnB, hipMemcpyHostToDevice));
+			HIP_OK(copy_wait(g->order.p, ordB.data(), 4ull * cnB, hipMemcpyHostToDevice, s));
 		}
 		hipEventRecord(g->ev_a, s);
 		if (launch_classB(g, b, cl, wsb, g->order.as<uint32_t>(), cnB, b->d_tid.as<uint32_t>() + cb, stats_on, s))
@@ -1429,13 +1507,13 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		hs_mark(HS_CARRY_B);
 		double td = now_ms();
 		uint32_t nh = 0;
-		HIP_OK(hipMemcpy(&nh, g->cnt.p, 4, hipMemcpyDeviceToHost));
-		HIP_OK(hipMemcpy(ro + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost));
-		HIP_OK(hipMemcpy(hit_off.data() + cb, g->hit_off.p, 4ull * cn, hipMemcpyDeviceToHost));
+		HIP_OK(copy_wait(&nh, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait(ro + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait(hit_off.data() + cb, g->hit_off.p, 4ull * cn, hipMemcpyDeviceToHost, s));
 		uint64_t base = hv.size();
 		hv.resize(base + nh);
 		if (nh)
-			HIP_OK(hipMemcpy(hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost));
+			HIP_OK(copy_wait(hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost, s));
 		for (uint32_t i = 0; i < cn; i++)
 			ro[cb + i].hit_off = base + hit_off[cb + i];
 		T.ms_d2h += now_ms() - td;
@@ -1467,9 +1545,9 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		if (g->vlen.ensure(4ull * m + 4, err, errn) || g->vso.ensure(8ull * m + 8, err, errn) ||
 		    g->vidx.ensure(4ull * m + 4, err, errn) || g->vtid.ensure(4ull * m + 4, err, errn))
 			return -1;
-		HIP_OK(hipMemcpy(g->vlen.p, vlen.data(), 4ull * m, hipMemcpyHostToDevice));
-		HIP_OK(hipMemcpy(g->vso.p, vso.data(), 8ull * m, hipMemcpyHostToDevice));
-		HIP_OK(hipMemcpy(g->vidx.p, vidx.data(), 4ull * m, hipMemcpyHostToDevice));
+		HIP_OK(copy_wait(g->vlen.p, vlen.data(), 4ull * m, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait(g->vso.p, vso.data(), 8ull * m, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait(g->vidx.p, vidx.data(), 4ull * m, hipMemcpyHostToDevice, s));
 		uint64_t rused = 0;
 		uint8_t *wsb = WS.as<uint8_t>();
 		const uint32_t *vcl = g->vlen.as<uint32_t>();
@@ -1481,8 +1559,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			vord[k] = k;
 			worst += vro[k].n_hit;
 		}
-		HIP_OK(hipMemcpy(g->order.p, vord.data(), 4ull * m, hipMemcpyHostToDevice));
-		HIP_OK(hipMemcpy(g->mrl.p, vmrl.data(), 4ull * m, hipMemcpyHostToDevice));
+		HIP_OK(copy_wait(g->order.p, vord.data(), 4ull * m, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait(g->mrl.p, vmrl.data(), 4ull * m, hipMemcpyHostToDevice, s));
 		if (g->hits.ensure(sizeof(dsb_hit_out_t) * worst + 4096, err, errn))
 			return -1;
 		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
@@ -1495,13 +1573,13 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		HIP_OK(hipGetLastError());
 		uint32_t nh = 0;
 		std::vector<uint32_t> voff(m);
-		HIP_OK(hipMemcpy(&nh, g->cnt.p, 4, hipMemcpyDeviceToHost));
-		HIP_OK(hipMemcpy(vro.data(), g->ro.p, sizeof(dsb_read_out_t) * m, hipMemcpyDeviceToHost));
-		HIP_OK(hipMemcpy(voff.data(), g->hit_off.p, 4ull * m, hipMemcpyDeviceToHost));
+		HIP_OK(copy_wait(&nh, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait(vro.data(), g->ro.p, sizeof(dsb_read_out_t) * m, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait(voff.data(), g->hit_off.p, 4ull * m, hipMemcpyDeviceToHost, s));
 		uint64_t base = hv.size();
 		hv.resize(base + nh);
 		if (nh)
-			HIP_OK(hipMemcpy(hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost));
+			HIP_OK(copy_wait(hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost, s));
 		for (uint32_t k = 0; k < m; k++) {
 			ro[deferred[k]] = vro[k];
 			ro[deferred[k]].hit_off = base + voff[k];
@@ -1511,7 +1589,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	*max_read_l = carry;
 	if (tl_bytes && getenv("DSB_TIMELINE")) {
 		std::vector<uint64_t> tl(tl_bytes / 8);
-		HIP_OK(hipMemcpy(tl.data(), g->stats.as<uint8_t>() + 8 * DSB_N_STATS, tl_bytes, hipMemcpyDeviceToHost));
+		HIP_OK(copy_wait(tl.data(), g->stats.as<uint8_t>() + 8 * DSB_N_STATS, tl_bytes, hipMemcpyDeviceToHost, s));
 		if (FILE *f = fopen(getenv("DSB_TIMELINE"), "wb")) {
 			fwrite(tl.data(), 8, tl.size(), f);
 			fclose(f);
@@ -1519,7 +1597,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	}
 	if (stats_on) {
 		unsigned long long st[DSB_N_STATS];
-		HIP_OK(hipMemcpy(st, g->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+		HIP_OK(copy_wait(st, g->stats.p, sizeof(st), hipMemcpyDeviceToHost, s));
 		for (int k = 0; k < DSB_N_STATS; k++) T.stats[k] = st[k];
 	}
 	return 0;

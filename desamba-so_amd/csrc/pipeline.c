@@ -483,8 +483,6 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 		snprintf(err, errn, "index not resident on a GPU");
 		return -1;
 	}
-	if (dsb_gpu_fit_contexts(ix, err, errn))
-		return -1;
 	pipe_t P;
 	memset(&P, 0, sizeof(P));
 	pipe_t *p = &P;
@@ -503,6 +501,9 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 	p->first_div = env_u64("DSB_PIPE_FIRST", 4);
 	p->tail_div = env_u64("DSB_PIPE_TAIL", 0);
 	if (p->first_div == 0) p->first_div = 1;
+	if (p->max_reads == 0) p->max_reads = 1;
+	if (dsb_gpu_fit_contexts(ix, p->max_reads, err, errn))
+		return -1;
 	p->depth = env_u64("DSB_PIPE_DEPTH", 2 + 2 * (uint64_t)n_dev);
 	if (p->max_reads == 0) p->max_reads = 1;
 	if (p->depth < 2) p->depth = 2;
