@@ -278,7 +278,7 @@ struct dsb_gpu_dev {
 	pthread_mutex_t umu;
 	void *pin[2] = {nullptr, nullptr};
 	size_t pin_cap[2] = {0, 0};
-	void *bounce = nullptr;   /* pinned bounce buffer of the waited copies (copy_wait), under the run lock */
+	void *bounce = nullptr;   /* pinned bounce buffer of the waited copies (copy_wait_g), under the run lock */
 	size_t bounce_cap = 0;
 	hipEvent_t pin_ev[2];
 	int pin_used[2] = {0, 0};
@@ -995,7 +995,6 @@ static hipError_t copy_wait_g(dsb_gpu_dev *g, void *dst, const void *src, size_t
 	}
 	return hipSuccess;
 }
-#define copy_wait(dst, src, n, k, s) copy_wait_g(g, (dst), (src), (n), (k), (s))
 
 /* The slow phases touch ~2% of the reads and leave most of the GPU idle: after resolve_f the
  * reads are split, the scoring of the rest runs on a second stream while the slow phases and
@@ -1014,7 +1013,7 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 					       g->cnt2.as<uint32_t>());
 	HIP_OK(hipGetLastError());
 	uint32_t c2[2] = {0, 0};
-	HIP_OK(copy_wait(c2, g->cnt2.p, 8, hipMemcpyDeviceToHost, s));
+	HIP_OK(copy_wait_g(g, c2, g->cnt2.p, 8, hipMemcpyDeviceToHost, s));
 	if (c2[0] + c2[1] != cn) {
 		snprintf(err, errn, "split: %u + %u reads for a chunk of %u", c2[0], c2[1], cn);
 		return -1;
@@ -1215,14 +1214,14 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 					vws_off[cb + i] += rbase;
 				rused += tot2;
 			}
-			HIP_OK(copy_wait(g->ws_off.p, vws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
-			HIP_OK(copy_wait(g->scale.p, vscale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait_g(g, g->ws_off.p, vws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait_g(g, g->scale.p, vscale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
 			std::vector<uint64_t> wo2;
 			uint64_t tw2 = seed_words(vlen, cb, sel.data(), sel.size(), l_ek, wo2, nullptr);
 			if (g->sel.ensure(4 * sel.size() + 4, err, errn) || g->wo2.ensure(8 * wo2.size() + 16, err, errn))
 				return -1;
-			HIP_OK(copy_wait(g->sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, s));
-			HIP_OK(copy_wait(g->wo2.p, wo2.data(), 8 * wo2.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait_g(g, g->sel.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait_g(g, g->wo2.p, wo2.data(), 8 * wo2.size(), hipMemcpyHostToDevice, s));
 			uint32_t m = (uint32_t)sel.size();
 			if (m == 0) {
 				snprintf(err, errn, "overflow reported by the phase kernels but no read carries the flag");
@@ -1239,8 +1238,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			/* the re-run went to the non-blocking stream: drain it before the (null-stream) copies */
 			HIP_OK(hipStreamSynchronize(s));
 			hash_ms(g, 1); /* re-runs are not timed */
-			HIP_OK(copy_wait(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
-			HIP_OK(copy_wait(vro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
+			HIP_OK(copy_wait_g(g, &n_over, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
+			HIP_OK(copy_wait_g(g, vro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
 		}
 		return 0;
 	};
@@ -1277,13 +1276,13 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			return -1;
 		if (!DSB_HSET_POOL && WS.p != ws_before) /* fresh bytes: no stale sp_set slot may carry a live tag */
 			HIP_OK(hipMemsetAsync(WS.p, 0, WS.cap, s));
-		HIP_OK(copy_wait(g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
-		HIP_OK(copy_wait(g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait_g(g, g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait_g(g, g->scale.p, scale.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
 		const uint32_t *cl = b->d_len.as<uint32_t>() + cb;
 		const uint64_t *cso = b->d_seq_off.as<uint64_t>() + cb;
 		/* length-sorted order (longest first) for the one-lane-per-read kernels */
 		const std::vector<uint32_t> &order = chunk_order(b, cb, ce);
-		HIP_OK(copy_wait(g->order.p, order.data(), 4ull * cn, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait_g(g, g->order.p, order.data(), 4ull * cn, hipMemcpyHostToDevice, s));
 		uint8_t *wsb = WS.as<uint8_t>();
 		hs_mark(HS_SETUP);
 		hipEventRecord(g->ev_a, s);
@@ -1301,8 +1300,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			uint64_t twB = seed_words(len, cb, order.data() + h, cn - h, l_ek, woB, &T.seed_positions);
 			if (g->woA.ensure(8 * woA.size() + 16, err, errn) || g->woB.ensure(8 * woB.size() + 16, err, errn))
 				return -1;
-			HIP_OK(copy_wait(g->woA.p, woA.data(), 8 * woA.size(), hipMemcpyHostToDevice, s));
-			HIP_OK(copy_wait(g->woB.p, woB.data(), 8 * woB.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait_g(g, g->woA.p, woA.data(), 8 * woA.size(), hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait_g(g, g->woB.p, woB.data(), 8 * woB.size(), hipMemcpyHostToDevice, s));
 			const uint32_t *oA = g->order.as<uint32_t>(), *oB = oA + h;
 			if (pipe_halves()) {
 				/* half A (longest reads) on the library stream, half B on the low-priority second
@@ -1385,7 +1384,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			}
 		} else {
 			tw = seed_words(len, cb, nullptr, cn, l_ek, word_off, &T.seed_positions);
-			HIP_OK(copy_wait(g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait_g(g, g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
 			T.n_launch_phase += 1;
 		}
 		if (tw && DSB_ISLAND_G == 0) {
@@ -1423,8 +1422,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		hs_mark(HS_PARTA);
 		HIP_OK(hipStreamSynchronize(s));
 		uint32_t n_over = 0;
-		HIP_OK(copy_wait(&n_over, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
-		HIP_OK(copy_wait(h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait_g(g, &n_over, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait_g(g, h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
 		hs_mark(HS_SYNC_A);
 		/* ---- max_read_l carry (src/cly.c:2953): prefix max over reads reaching the update; a
 		 * streamed batch takes its carry-in from the batch before it (possibly on another GPU)
@@ -1485,7 +1484,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		}
 		if (ce == n && hooks && hooks->carry_out)
 			hooks->carry_out(hooks->ctx, carry);
-		HIP_OK(copy_wait(g->mrl.p, mrl.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait_g(g, g->mrl.p, mrl.data() + cb, 4ull * cn, hipMemcpyHostToDevice, s));
 		if (g->hits.ensure(sizeof(dsb_hit_out_t) * worst + 4096, err, errn))
 			return -1;
 		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
@@ -1497,7 +1496,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				if (!h_ro[cb + i].status)
 					ordB.push_back(i);
 			cnB = (uint32_t)ordB.size();
-			HIP_OK(copy_wait(g->order.p, ordB.data(), 4ull * cnB, hipMemcpyHostToDevice, s));
+			HIP_OK(copy_wait_g(g, g->order.p, ordB.data(), 4ull * cnB, hipMemcpyHostToDevice, s));
 		}
 		hipEventRecord(g->ev_a, s);
 		if (launch_classB(g, b, cl, wsb, g->order.as<uint32_t>(), cnB, b->d_tid.as<uint32_t>() + cb, stats_on, s))
@@ -1507,13 +1506,13 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		hs_mark(HS_CARRY_B);
 		double td = now_ms();
 		uint32_t nh = 0;
-		HIP_OK(copy_wait(&nh, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
-		HIP_OK(copy_wait(ro + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
-		HIP_OK(copy_wait(hit_off.data() + cb, g->hit_off.p, 4ull * cn, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait_g(g, &nh, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait_g(g, ro + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait_g(g, hit_off.data() + cb, g->hit_off.p, 4ull * cn, hipMemcpyDeviceToHost, s));
 		uint64_t base = hv.size();
 		hv.resize(base + nh);
 		if (nh)
-			HIP_OK(copy_wait(hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost, s));
+			HIP_OK(copy_wait_g(g, hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost, s));
 		for (uint32_t i = 0; i < cn; i++)
 			ro[cb + i].hit_off = base + hit_off[cb + i];
 		T.ms_d2h += now_ms() - td;
@@ -1545,9 +1544,9 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		if (g->vlen.ensure(4ull * m + 4, err, errn) || g->vso.ensure(8ull * m + 8, err, errn) ||
 		    g->vidx.ensure(4ull * m + 4, err, errn) || g->vtid.ensure(4ull * m + 4, err, errn))
 			return -1;
-		HIP_OK(copy_wait(g->vlen.p, vlen.data(), 4ull * m, hipMemcpyHostToDevice, s));
-		HIP_OK(copy_wait(g->vso.p, vso.data(), 8ull * m, hipMemcpyHostToDevice, s));
-		HIP_OK(copy_wait(g->vidx.p, vidx.data(), 4ull * m, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait_g(g, g->vlen.p, vlen.data(), 4ull * m, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait_g(g, g->vso.p, vso.data(), 8ull * m, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait_g(g, g->vidx.p, vidx.data(), 4ull * m, hipMemcpyHostToDevice, s));
 		uint64_t rused = 0;
 		uint8_t *wsb = WS.as<uint8_t>();
 		const uint32_t *vcl = g->vlen.as<uint32_t>();
@@ -1559,8 +1558,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			vord[k] = k;
 			worst += vro[k].n_hit;
 		}
-		HIP_OK(copy_wait(g->order.p, vord.data(), 4ull * m, hipMemcpyHostToDevice, s));
-		HIP_OK(copy_wait(g->mrl.p, vmrl.data(), 4ull * m, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait_g(g, g->order.p, vord.data(), 4ull * m, hipMemcpyHostToDevice, s));
+		HIP_OK(copy_wait_g(g, g->mrl.p, vmrl.data(), 4ull * m, hipMemcpyHostToDevice, s));
 		if (g->hits.ensure(sizeof(dsb_hit_out_t) * worst + 4096, err, errn))
 			return -1;
 		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
@@ -1573,13 +1572,13 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		HIP_OK(hipGetLastError());
 		uint32_t nh = 0;
 		std::vector<uint32_t> voff(m);
-		HIP_OK(copy_wait(&nh, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
-		HIP_OK(copy_wait(vro.data(), g->ro.p, sizeof(dsb_read_out_t) * m, hipMemcpyDeviceToHost, s));
-		HIP_OK(copy_wait(voff.data(), g->hit_off.p, 4ull * m, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait_g(g, &nh, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait_g(g, vro.data(), g->ro.p, sizeof(dsb_read_out_t) * m, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait_g(g, voff.data(), g->hit_off.p, 4ull * m, hipMemcpyDeviceToHost, s));
 		uint64_t base = hv.size();
 		hv.resize(base + nh);
 		if (nh)
-			HIP_OK(copy_wait(hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost, s));
+			HIP_OK(copy_wait_g(g, hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost, s));
 		for (uint32_t k = 0; k < m; k++) {
 			ro[deferred[k]] = vro[k];
 			ro[deferred[k]].hit_off = base + voff[k];
@@ -1589,7 +1588,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	*max_read_l = carry;
 	if (tl_bytes && getenv("DSB_TIMELINE")) {
 		std::vector<uint64_t> tl(tl_bytes / 8);
-		HIP_OK(copy_wait(tl.data(), g->stats.as<uint8_t>() + 8 * DSB_N_STATS, tl_bytes, hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait_g(g, tl.data(), g->stats.as<uint8_t>() + 8 * DSB_N_STATS, tl_bytes, hipMemcpyDeviceToHost, s));
 		if (FILE *f = fopen(getenv("DSB_TIMELINE"), "wb")) {
 			fwrite(tl.data(), 8, tl.size(), f);
 			fclose(f);
@@ -1597,7 +1596,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	}
 	if (stats_on) {
 		unsigned long long st[DSB_N_STATS];
-		HIP_OK(copy_wait(st, g->stats.p, sizeof(st), hipMemcpyDeviceToHost, s));
+		HIP_OK(copy_wait_g(g, st, g->stats.p, sizeof(st), hipMemcpyDeviceToHost, s));
 		for (int k = 0; k < DSB_N_STATS; k++) T.stats[k] = st[k];
 	}
 	return 0;
