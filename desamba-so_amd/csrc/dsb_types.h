@@ -79,11 +79,14 @@ typedef struct {
 	/* seeding sp_set pool (GPU build, dsb_classify.h DSB_HSET_POOL): hpool_nx partitions (one per
 	 * XCD) of hpool_part wave-sized sets (DSB_HSET_WAVE_U64 words each), an owner flag and a
 	 * generation base per set; hpool_part is a power of two >= the waves an XCD can hold at once,
-	 * so an acquiring wave always finds one in its XCD's partition (dsb_kern.h) */
+	 * so an acquiring wave always finds one in its XCD's partition (dsb_kern.h).  hpool_fenced:
+	 * the XCC ids the device's waves report were not exactly 0..hpool_nx-1 at load (or the XCC
+	 * count was unknown), so one partition is used and every hand-over is an agent-scope
+	 * release / acquire (kernels.hip dev_init). */
 	uint64_t *hpool;
 	uint32_t *hpool_own;
 	uint64_t *hpool_gen;
-	uint32_t hpool_part, hpool_nx;
+	uint32_t hpool_part, hpool_nx, hpool_fenced;
 } dsb_dindex_t;
 
 /* Output record per hit (what output_one_result_sam needs, cly_mt.c:229-327) */

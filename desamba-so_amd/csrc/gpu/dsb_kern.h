@@ -534,13 +534,18 @@ static_assert(DSB_HSET_WAVE_U64 == (uint64_t)DSB_HSET_SLOT_U64 * DSB_HSET_SLOTS 
 __device__ __forceinline__ uint32_t dsb_hpool_acquire(const dsb_dindex_t *ix, uint32_t start, uint64_t *gen_base)
 {
 	uint32_t s = 0, glo = 0, ghi = 0;
+	const int fenced = ix->hpool_fenced; /* uniform */
 	if (dsb_lane() == 0) {
-		uint32_t xcc = ((uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xfu) % ix->hpool_nx; /* HW_REG_XCC_ID */
+		/* HW_REG_XCC_ID: dev_init checked that the device's waves report exactly 0..hpool_nx-1
+		 * (else hpool_nx is 1 and the hand-over fenced) */
+		uint32_t xcc = ((uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0xfu) % ix->hpool_nx;
 		uint32_t mask = ix->hpool_part - 1, base = xcc * ix->hpool_part, q = start & mask;
 		for (;;) {
 			uint32_t expect = 0;
-			if (__hip_atomic_compare_exchange_strong(ix->hpool_own + base + q, &expect, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-								 __HIP_MEMORY_SCOPE_AGENT))
+			if (fenced ? __hip_atomic_compare_exchange_strong(ix->hpool_own + base + q, &expect, 1u, __ATOMIC_ACQUIRE,
+									  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+				   : __hip_atomic_compare_exchange_strong(ix->hpool_own + base + q, &expect, 1u, __ATOMIC_RELAXED,
+									  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
 				break;
 			q = (q + 1) & mask;
 		}
@@ -550,13 +555,18 @@ __device__ __forceinline__ uint32_t dsb_hpool_acquire(const dsb_dindex_t *ix, ui
 		ghi = (uint32_t)(g >> 32);
 	}
 	*gen_base = ((uint64_t)(uint32_t)dsb_wshfl((int)ghi, 0) << 32) | (uint32_t)dsb_wshfl((int)glo, 0);
+	if (fenced) /* every lane: no stale line of the set in this CU's L1 / this XCD's L2 */
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 	return (uint32_t)dsb_wshfl((int)s, 0);
 }
 /* the next holder's tags start past `last_gen`, the wave's highest generation */
 __device__ __forceinline__ void dsb_hpool_release(const dsb_dindex_t *ix, uint32_t s, uint64_t gen_base, uint32_t last_gen, uint32_t dbg)
 {
 	uint32_t top = (uint32_t)dsb_wmax((int)last_gen);
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); /* keeps the slot stores above the wait */
+	if (ix->hpool_fenced) /* every lane's slot stores written back past this XCD's L2 */
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+	else
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); /* keeps the slot stores above the wait */
 	__builtin_amdgcn_s_waitcnt(0);                        /* every lane's slot stores are in the L2 */
 	if (dsb_lane() == 0) {
 		if (!(dbg & DSB_DBG_POOL_NOGEN)) /* tests: keep the base, so the next holder meets live slots */

@@ -29,6 +29,9 @@
 
 #include "dsb_kern.h"
 #include "dsb_debug.h"
+#ifndef DSB_TEST_HOOKS /* 1: the test build lib/libdesamba_test.so (the env-reachable test hooks below) */
+#define DSB_TEST_HOOKS 0
+#endif
 static_assert(DSB_ST_N <= DSB_ST_STRIDE, "work counters per phase");
 
 #define HIP_OK(x)                                                                                    \
@@ -228,6 +231,7 @@ __global__ void k_selftest_sort(dsb_chain_t *chains, dsb_chain_t *tmp, uint32_t 
 }
 
 /* ------------------------------------------------------------------ host side */
+#define DSB_BOUNCE_BYTES ((size_t)32 << 20) /* pinned bounce buffer per context (copy_wait_g) */
 /* device buffer that grows (persistent per device context; calls are serialised) */
 struct dbuf {
 	void *p = nullptr;
@@ -263,12 +267,11 @@ struct dsb_gpu_dev {
 	hipStream_t stream;
 	hipStream_t stream2;     /* scoring of the reads that skip slow seeding, beside the slow phases */
 	hipEvent_t ev_a, ev_b, ev_fork, ev_r0, ev_r1;
-	hipEvent_t pev[2][DSB_PH_N + 1][2]; /* pipelined halves: k_seed and each phase launch, start / end */
 	pthread_mutex_t mu;
 	dsb_dindex_t h;          /* host copy holding device pointers */
 	dsb_dindex_t *d;         /* device copy */
 	std::vector<void *> allocs;
-	dbuf ws_off, scale, ws, wsr, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2, woA, woB;
+	dbuf ws_off, scale, ws, wsr, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2;
 	dbuf vlen, vso, vidx, vtid; /* the deferred overflow re-runs of a batch (batch_run) */
 	hipEvent_t evh[2][2];    /* k_hash_lds before the scoring launch, per stream (launch_phase) */
 	int evh_used[2] = {0, 0};
@@ -309,6 +312,31 @@ extern "C" int dsb_gpu_device_count(void)
 	return n;
 }
 
+/* the XCC ids (HW_REG_XCC_ID) the waves of this device report, as a bit set */
+__global__ __launch_bounds__(64) void k_xcc_probe(uint32_t *seen)
+{
+	if (threadIdx.x == 0)
+		atomicOr(seen, 1u << ((uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) & 0x1fu));
+}
+
+#if DSB_TEST_HOOKS /* tests: the fenced sp_set pool hand-over on any device */
+#define DSB_TEST_POOL_FENCED() (getenv("DSB_TEST_POOL_FENCED") != NULL)
+#else
+#define DSB_TEST_POOL_FENCED() 0
+#endif
+
+static int xcc_ids_seen(uint32_t *out, char *err, size_t errn)
+{
+	uint32_t *d = nullptr;
+	HIP_OK(hipMalloc(&d, 4));
+	HIP_OK(hipMemset(d, 0, 4));
+	k_xcc_probe<<<1 << 15, 64>>>(d); /* 32k one-wave workgroups: every CU of every XCC */
+	HIP_OK(hipGetLastError());
+	HIP_OK(hipMemcpy(out, d, 4, hipMemcpyDeviceToHost));
+	HIP_OK(hipFree(d));
+	return 0;
+}
+
 /* A device context: streams, events, workspace, and the index tables — its own upload, or
  * those of `share`, an earlier context on the same GPU (several contexts per GPU let batches of
  * one read_classify call run their kernels side by side, each context with its own workspace). */
@@ -326,6 +354,9 @@ static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu
 		HIP_OK(hipEventCreateWithFlags(&g->pin_ev[k], hipEventDisableTiming));
 	HIP_OK(hipEventCreate(&g->ev_a));
 	HIP_OK(hipEventCreate(&g->ev_b));
+	/* the pinned bounce buffer of the waited copies (copy_wait_g), once per context */
+	HIP_OK(hipHostMalloc(&g->bounce, DSB_BOUNCE_BYTES, hipHostMallocDefault));
+	g->bounce_cap = DSB_BOUNCE_BYTES;
 	{ /* the split-off scoring yields to the slow phases */
 		int least = 0, greatest = 0;
 		HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -337,10 +368,6 @@ static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu
 	for (int k = 0; k < 2; k++)
 		for (int e = 0; e < 2; e++)
 			HIP_OK(hipEventCreate(&g->evh[k][e]));
-	for (int k = 0; k < 2; k++)
-		for (int ph = 0; ph <= DSB_PH_N; ph++)
-			for (int e = 0; e < 2; e++)
-				HIP_OK(hipEventCreate(&g->pev[k][ph][e]));
 	if (share) { /* read-only tables: one copy per GPU */
 		g->h = share->h;
 		g->d = share->d;
@@ -391,9 +418,20 @@ static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu
 		 * no slot matches a tag before its first writer (generation 0 is never used) */
 		hipDeviceProp_t prop;
 		HIP_OK(hipGetDeviceProperties(&prop, device));
-		int nx = 1;
+		int nx = 0, fenced = 0;
+		uint32_t seen = 0;
 		if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, device) != hipSuccess || nx < 1)
+			nx = 0;
+		if (xcc_ids_seen(&seen, err, errn))
+			return -1;
+		/* the partition of a wave is its XCC id modulo hpool_nx: correct only when the ids are
+		 * exactly 0..nx-1 (one L2 per partition); otherwise one partition with fenced hand-overs */
+		if (nx < 1 || nx > 16 || seen != (nx >= 32 ? ~0u : (1u << nx) - 1) || DSB_TEST_POOL_FENCED()) {
+			fprintf(stderr, "[dsb] device %d: %d XCCs reported, XCC ids seen %#x: sp_set pool hand-over fenced\n",
+				device, nx, seen);
 			nx = 1;
+			fenced = 1;
+		}
 		uint64_t per_cu = DSB_MAX(32u, (uint32_t)prop.maxThreadsPerMultiProcessor / 64u);
 		uint64_t waves = ((uint64_t)prop.multiProcessorCount + nx - 1) / nx * per_cu, part = 1;
 		while (part < waves)
@@ -411,6 +449,7 @@ static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu
 		h.hpool_own = (uint32_t *)((uint8_t *)p + 8 * n);
 		h.hpool_part = (uint32_t)part;
 		h.hpool_nx = (uint32_t)nx;
+		h.hpool_fenced = (uint32_t)fenced;
 	}
 	const dsb_dindex_t *dptr;
 	if (upload(g, &h, 1, &dptr, err, errn)) return -1;
@@ -525,7 +564,7 @@ static void dev_free(dsb_gpu_dev *g)
 	for (void *p : g->allocs)
 		hipFree(p);
 	dbuf *bs[] = {&g->ws_off, &g->scale, &g->ws, &g->wsr, &g->order, &g->word_off, &g->ro, &g->mrl, &g->hits,
-		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2, &g->woA, &g->woB};
+		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2};
 	for (dbuf *b : bs)
 		b->release();
 	hipEventDestroy(g->ev_a);
@@ -533,6 +572,9 @@ static void dev_free(dsb_gpu_dev *g)
 	hipEventDestroy(g->ev_fork);
 	hipEventDestroy(g->ev_r0);
 	hipEventDestroy(g->ev_r1);
+	for (int k = 0; k < 2; k++)
+		for (int e = 0; e < 2; e++)
+			hipEventDestroy(g->evh[k][e]);
 	hipStreamDestroy(g->stream2);
 	hipStreamDestroy(g->stream);
 	pthread_mutex_destroy(&g->mu);
@@ -714,20 +756,23 @@ static uint64_t seed_words(const std::vector<uint32_t> &len, uint64_t cb, const 
 	return tw;
 }
 
-/* diagnostics / experiments: DSB_WAVE_DBG bits (dsb_classify.h) */
+/* Test hooks (DSB_WAVE_DBG bits other than the timeline, DSB_WAVE_PHASES, DSB_TEST_SCALE0) exist
+ * only in the test build of the library (lib/libdesamba_test.so, -DDSB_TEST_HOOKS=1): they force
+ * staging overflows, sequential wave-loop variants, lane-per-read phases or stale sp_set pool
+ * generations.  The production library ignores them. */
 static uint32_t wave_dbg(void)
 {
 	const char *e = getenv("DSB_WAVE_DBG");
 	uint32_t d = e ? (uint32_t)strtoul(e, NULL, 0) : 0;
-	return d;
+	return DSB_TEST_HOOKS ? d : (d & DSB_DBG_TIMELINE); /* the timeline is a read-only dev tool (DSB_TL builds) */
 }
 
-/* phases run with one wavefront per read (DSB_WAVE_PHASES overrides, for diagnostics) */
+/* phases run with one wavefront per read (DSB_WAVE_PHASES overrides in the test build) */
 static uint32_t wave_phases(void)
 {
-	const char *e = getenv("DSB_WAVE_PHASES");
-	if (e)
-		return (uint32_t)strtoul(e, NULL, 0);
+	if (DSB_TEST_HOOKS)
+		if (const char *e = getenv("DSB_WAVE_PHASES"))
+			return (uint32_t)strtoul(e, NULL, 0);
 	return (1u << DSB_PH_FAST0) | (1u << DSB_PH_FAST1) | (1u << DSB_PH_RESOLVE_F) | (1u << DSB_PH_SLOW0) |
 	       (1u << DSB_PH_RESOLVE_S0) | (1u << DSB_PH_SLOW1) | (1u << DSB_PH_RESOLVE_S1) | (1u << DSB_PH_DELA);
 }
@@ -913,30 +958,6 @@ __global__ __launch_bounds__(64) void k_split(const uint32_t *__restrict__ len, 
 		rest_list[br + (uint32_t)__builtin_popcountll(mr & lt)] = r;
 }
 
-static int split_seed(void)
-{
-	static int v = -1;
-	if (v < 0)
-		v = (DSB_ISLAND_G > 0 || getenv("DSB_NO_SPLIT_SEED")) ? 0 : 1; /* k_island_g: no k_seed to overlap */
-	return v;
-}
-
-/* Pipelined halves (DSB_PIPE=1; off by default): the chunk's reads are split in two halves
- * (longest first), each runs k_seed and every phase of part A in order on a stream of its own,
- * B's k_seed starting when A's ends, so that B's bandwidth-bound k_seed runs beside A's
- * latency-bound phases and each phase kernel's tail is filled by the other half.  Measured r02
- * (C1, one box): 596.5k vs 591.4k reads/s, within box-to-box spread — every phase kernel already
- * fills the wave slots, so co-running kernels trade slots rather than add throughput — and the
- * per-kernel launch times then overlap, so the roofline's launch durations stay with the
- * phase-by-phase order. */
-static int pipe_halves(void)
-{
-	static int v = -1;
-	if (v < 0)
-		v = getenv("DSB_PIPE") ? 1 : 0;
-	return v;
-}
-
 /* The split of part A (run_split): after resolve_f the reads that still need slow seeding run
  * their slow phases on the library stream while the scoring of every other read runs on the
  * second stream.  On by default since round 4: on the C2 proxy the slow phases are ~14% of a step
@@ -958,22 +979,20 @@ static int split_slow(void)
  * the context's pinned bounce buffer.  A pageable copy (hipMemcpy, or hipMemcpyAsync on the
  * stream) waited for the other context's kernels on the GPU: 60-150 ms inside a 250-450 ms
  * read_classify call (the first batch's results, measured with DSB_HOST_TIMING); a pinned copy is
- * a DMA on this stream only.  Large copies go in bounce-sized pieces. */
+ * a DMA on this stream only.  The bounce buffer has a fixed size, allocated once per context
+ * (growing it would hipHostFree, which synchronises the whole device: the other context's kernels);
+ * larger copies go in bounce-sized pieces. */
 static hipError_t copy_wait_g(dsb_gpu_dev *g, void *dst, const void *src, size_t n, hipMemcpyKind k, hipStream_t s)
 {
 	if (n == 0)
 		return hipSuccess;
-	const size_t want = std::min(n, (size_t)256 << 20);
-	if (g->bounce_cap < want) {
-		if (g->bounce)
-			hipHostFree(g->bounce);
-		g->bounce = nullptr;
-		g->bounce_cap = 0;
-		size_t c = std::max(want, (size_t)16 << 20);
-		hipError_t e = hipHostMalloc(&g->bounce, c, hipHostMallocDefault);
-		if (e != hipSuccess)
+	if (!g->bounce) {
+		hipError_t e = hipHostMalloc(&g->bounce, DSB_BOUNCE_BYTES, hipHostMallocDefault);
+		if (e != hipSuccess) {
+			g->bounce = nullptr;
 			return e;
-		g->bounce_cap = c;
+		}
+		g->bounce_cap = DSB_BOUNCE_BYTES;
 	}
 	for (size_t o = 0; o < n; o += g->bounce_cap) {
 		size_t m = std::min(g->bounce_cap, n - o);
@@ -1142,11 +1161,12 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	HIP_OK(hipMemsetAsync(g->stats.p, 0, 8 * DSB_N_STATS + tl_bytes, s));
 	/* k_seed's probe counters (stats mode 1) go to the island phase's ek1 / ek2 slots */
 	unsigned long long *sst = stats_on == 1 ? g->stats.as<unsigned long long>() : nullptr;
-	/* DSB_TEST_SCALE0 (tests): start below the default capacities so that reads overflow and
+	/* DSB_TEST_SCALE0 (test build only): start below the default capacities so that reads overflow and
 	 * take the re-run path */
 	uint32_t scale0 = DSB_SCALE_UNIT;
-	if (const char *e = getenv("DSB_TEST_SCALE0"))
-		scale0 = (uint32_t)DSB_MAX(1, atoi(e));
+	if (DSB_TEST_HOOKS)
+		if (const char *e = getenv("DSB_TEST_SCALE0"))
+			scale0 = (uint32_t)DSB_MAX(1, atoi(e));
 	std::vector<uint32_t> scale(n, scale0);
 	std::vector<uint64_t> ws_off(n);
 	std::vector<dsb_read_out_t> h_ro(n);
@@ -1289,115 +1309,20 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		k_encode<<<cn, 256, 0, s>>>(b->seq.as<uint8_t>(), cso, cl, g->ws_off.as<uint64_t>(), wsb, nullptr, cn);
 		T.ms_encode += ev_ms(g);
 		HIP_OK(hipGetLastError());
-		int ph0 = 0; /* first phase still to run */
-		uint64_t tw = 0;
-		if (split_seed() && cn >= 2048) {
-			/* the island scan of the longer half runs on the second stream while k_seed probes the
-			 * shorter half (the island scan keeps few waves in flight, k_seed is bandwidth work) */
-			uint32_t h = cn / 2;
-			std::vector<uint64_t> woA, woB;
-			uint64_t twA = seed_words(len, cb, order.data(), h, l_ek, woA, &T.seed_positions);
-			uint64_t twB = seed_words(len, cb, order.data() + h, cn - h, l_ek, woB, &T.seed_positions);
-			if (g->woA.ensure(8 * woA.size() + 16, err, errn) || g->woB.ensure(8 * woB.size() + 16, err, errn))
-				return -1;
-			HIP_OK(copy_wait_g(g, g->woA.p, woA.data(), 8 * woA.size(), hipMemcpyHostToDevice, s));
-			HIP_OK(copy_wait_g(g, g->woB.p, woB.data(), 8 * woB.size(), hipMemcpyHostToDevice, s));
-			const uint32_t *oA = g->order.as<uint32_t>(), *oB = oA + h;
-			if (pipe_halves()) {
-				/* half A (longest reads) on the library stream, half B on the low-priority second
-				 * stream; phase launches interleaved so that both queues hold work early */
-				HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
-				hipEventRecord(g->ev_fork, s);
-				HIP_OK(hipStreamWaitEvent(g->stream2, g->ev_fork, 0));
-				hipStream_t hs[2] = {s, g->stream2};
-				const uint32_t *ho[2] = {oA, oB};
-				uint32_t hm[2] = {h, cn - h};
-				uint64_t htw[2] = {twA, twB};
-				const uint64_t *hwo[2] = {g->woA.as<uint64_t>(), g->woB.as<uint64_t>()};
-				for (int k = 0; k < 2; k++) {
-					/* B's k_seed starts when A's has finished: it then streams beside A's
-					 * latency-bound phases instead of sharing HBM with A's k_seed */
-					if (k == 1)
-						HIP_OK(hipStreamWaitEvent(hs[1], g->pev[0][0][1], 0));
-					hipEventRecord(g->pev[k][0][0], hs[k]);
-					if (htw[k])
-						k_seed<<<(uint32_t)((htw[k] * 64 + 255) / 256), 256, 0, hs[k]>>>(
-							g->d, cl, g->ws_off.as<uint64_t>(), wsb, hwo[k], ho[k], hm[k], htw[k], sst);
-					hipEventRecord(g->pev[k][0][1], hs[k]);
-				}
-				for (int ph = 0; ph < DSB_PH_N; ph++)
-					for (int k = 0; k < 2; k++) {
-						hipEventRecord(g->pev[k][ph + 1][0], hs[k]);
-						launch_phase(g, ph, stats_on, cl, wsb, ho[k], hm[k], hs[k]);
-						hipEventRecord(g->pev[k][ph + 1][1], hs[k]);
-					}
-				HIP_OK(hipGetLastError());
-				hipEventRecord(g->ev_r1, g->stream2);
-				HIP_OK(hipStreamWaitEvent(s, g->ev_r1, 0));
-				hipEventRecord(g->ev_b, s);
-				HIP_OK(hipEventSynchronize(g->ev_b));
-				/* wall accounting: k_seed of half A, then everything up to the join; per-phase
-				 * times are the sums of both halves' (overlapping) launch durations */
-				float f = 0;
-				hipEventElapsedTime(&f, g->pev[0][0][0], g->pev[0][0][1]);
-				T.ms_seed += f;
-				hipEventElapsedTime(&f, g->pev[0][0][1], g->ev_b);
-				T.ms_classA += f;
-				for (int ph = 0; ph < DSB_PH_N; ph++)
-					for (int k = 0; k < 2; k++) {
-						hipEventElapsedTime(&f, g->pev[k][ph + 1][0], g->pev[k][ph + 1][1]);
-						T.ms_phase[ph] += f;
-					}
-				T.n_launch_dela += 2;
-				T.n_launch_phase += 2;
-				ph0 = DSB_PH_N;
-			} else {
-			hipEventRecord(g->ev_a, s);
-			if (twA)
-				k_seed<<<(uint32_t)((twA * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
-											      g->woA.as<uint64_t>(), oA, h, twA, sst);
-			hipEventRecord(g->ev_fork, s);
-			HIP_OK(hipStreamWaitEvent(g->stream2, g->ev_fork, 0));
-			hipEventRecord(g->ev_r0, g->stream2);
-			launch_phase(g, DSB_PH_ISLAND, stats_on, cl, wsb, oA, h, g->stream2);
-			hipEventRecord(g->ev_r1, g->stream2);
-			if (twB)
-				k_seed<<<(uint32_t)((twB * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
-											      g->woB.as<uint64_t>(), oB, cn - h, twB, sst);
-			HIP_OK(hipGetLastError());
-			hipEventRecord(g->ev_b, s);
-			HIP_OK(hipEventSynchronize(g->ev_b));
-			float ms_s = 0;
-			hipEventElapsedTime(&ms_s, g->ev_a, g->ev_b);
-			T.ms_seed += ms_s;
-			hipEventRecord(g->ev_a, s);
-			launch_phase(g, DSB_PH_ISLAND, stats_on, cl, wsb, oB, cn - h);
-			HIP_OK(hipStreamWaitEvent(s, g->ev_r1, 0));
-			float ms_i = ev_ms(g), ms_ia = 0;
-			hipEventElapsedTime(&ms_ia, g->ev_r0, g->ev_r1);
-			T.ms_phase[DSB_PH_ISLAND] += ms_i; /* the wall time after k_seed; island A overlapped it */
-			T.ms_classA += ms_i;
-			(void)ms_ia;
-			HIP_OK(hipGetLastError());
-			ph0 = DSB_PH_ISLAND + 1;
-			T.n_launch_phase += 1;
-			}
-		} else {
-			tw = seed_words(len, cb, nullptr, cn, l_ek, word_off, &T.seed_positions);
+		/* k-mer positions (both strands) of the reads the island scan covers */
+		uint64_t tw = seed_words(len, cb, nullptr, cn, l_ek, word_off, &T.seed_positions);
+		T.n_launch_phase += 1;
+		if (tw && DSB_ISLAND_G == 0) { /* the rounds-1/2 form: k_seed's exist bits, then a two-lane island scan */
 			HIP_OK(copy_wait_g(g, g->word_off.p, word_off.data(), 8ull * (cn + 1), hipMemcpyHostToDevice, s));
-			T.n_launch_phase += 1;
-		}
-		if (tw && DSB_ISLAND_G == 0) {
 			hipEventRecord(g->ev_a, s);
 			k_seed<<<(uint32_t)((tw * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
 										     g->word_off.as<uint64_t>(), nullptr, cn, tw, sst);
 			T.ms_seed += ev_ms(g);
 			HIP_OK(hipGetLastError());
 		}
-		if (ph0 < DSB_PH_N)
-			HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
+		HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
 		/* island, fast seeding, resolve: every read */
-		for (int ph = ph0; ph < DSB_PH_N; ph++) {
+		for (int ph = 0; ph < DSB_PH_N; ph++) {
 			hipEventRecord(g->ev_a, s);
 			launch_phase(g, ph, stats_on, cl, wsb, g->order.as<uint32_t>(), cn);
 			float ms = ev_ms(g);
@@ -1541,8 +1466,13 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			vro[k] = ro[r]; /* part A's result: the overflow flag set */
 			vmrl[k] = mrl[r];
 		}
+		/* the order / carry / per-read arrays are sized per chunk elsewhere: m (every chunk's
+		 * deferred reads) may exceed the largest chunk */
 		if (g->vlen.ensure(4ull * m + 4, err, errn) || g->vso.ensure(8ull * m + 8, err, errn) ||
-		    g->vidx.ensure(4ull * m + 4, err, errn) || g->vtid.ensure(4ull * m + 4, err, errn))
+		    g->vidx.ensure(4ull * m + 4, err, errn) || g->vtid.ensure(4ull * m + 4, err, errn) ||
+		    g->order.ensure(4ull * m + 4, err, errn) || g->mrl.ensure(4ull * m + 4, err, errn) ||
+		    g->ws_off.ensure(8ull * m + 8, err, errn) || g->scale.ensure(4ull * m + 4, err, errn) ||
+		    g->ro.ensure(sizeof(dsb_read_out_t) * m + 64, err, errn) || g->hit_off.ensure(4ull * m + 4, err, errn))
 			return -1;
 		HIP_OK(copy_wait_g(g, g->vlen.p, vlen.data(), 4ull * m, hipMemcpyHostToDevice, s));
 		HIP_OK(copy_wait_g(g, g->vso.p, vso.data(), 8ull * m, hipMemcpyHostToDevice, s));

@@ -29,6 +29,9 @@
 #include <sys/mman.h>
 #include "dsb_host.h"
 #include "pipeline.h"
+#ifndef DSB_TEST_HOOKS
+#define DSB_TEST_HOOKS 0 /* lib/libdesamba_test.so: -DDSB_TEST_HOOKS=1 */
+#endif
 #include "gpu/dsb_gpu.h"
 
 typedef struct pbatch {
@@ -209,7 +212,7 @@ static void *stager(void *arg)
 	for (;;) {
 		pthread_mutex_lock(&p->mu);
 		/* at most two batches per GPU between staging and classified: one classifying, one staged;
-		 * DSB_TEST_ROUND_ROBIN (tests): batch k goes to GPU context k mod n */
+		 * DSB_TEST_ROUND_ROBIN (test build of the library): batch k goes to GPU context k mod n */
 		while (!p->failed && (p->runq_n[slot] >= 2 || (!p->parsed_head && !p->parse_done) ||
 				      (p->round_robin && p->parsed_head && p->parsed_head->seq % (uint64_t)p->n_dev != (uint64_t)slot)))
 			pthread_cond_wait(&p->cv, &p->mu);
@@ -495,7 +498,7 @@ int dsb_pipeline_classify(dsb_index *ix, dsb_pool *pool, const char *text, uint6
 	p->carry0 = *max_read_l;
 	pthread_mutex_init(&p->mu, NULL);
 	pthread_cond_init(&p->cv, NULL);
-	p->round_robin = env_u64("DSB_TEST_ROUND_ROBIN", 0) != 0;
+	p->round_robin = DSB_TEST_HOOKS && env_u64("DSB_TEST_ROUND_ROBIN", 0) != 0; /* test build only */
 	p->max_reads = env_u64("DSB_PIPE_READS", 100000); /* measured (C2 proxy, 100k reads): 25k / 50k / 100k -> 278k / 292k / 317k reads/s */
 	p->max_bases = env_u64("DSB_PIPE_MBP", 400) * 1000000ull;
 	p->first_div = env_u64("DSB_PIPE_FIRST", 4);

@@ -63,3 +63,26 @@ def test_load_index_fails_loudly_without_gpu(pyd, fixture_index):
     assert r.returncode != 0
     assert "LOADED" not in r.stdout
     assert "load_index" in r.stderr
+
+
+TEST_LIB = os.path.join(ROOT, "desamba-so_amd", "lib", "libdesamba_test.so")
+HOOK_ENV = ("DSB_TEST_SCALE0", "DSB_TEST_ROUND_ROBIN", "DSB_WAVE_PHASES")
+
+
+def _strings(path):
+    with open(path, "rb") as f:
+        return set(re.findall(rb"[\x20-\x7e]{6,}", f.read()))
+
+
+def test_test_hooks_only_in_the_test_build():
+    """The env-reachable test hooks (forced overflows, lane-per-read phases, batch-to-context
+    order) are compiled into lib/libdesamba_test.so only; the production library does not even
+    read those variables (kernels.hip / pipeline.c DSB_TEST_HOOKS)."""
+    if not os.path.exists(TEST_LIB):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "desamba-so_amd")], check=True, timeout=900)
+    prod, test = _strings(LIB), _strings(TEST_LIB)
+    for name in HOOK_ENV:
+        assert name.encode() not in prod, name
+        assert name.encode() in test, name
+    out = subprocess.run(["nm", "-D", "--defined-only", TEST_LIB], capture_output=True, text=True, check=True).stdout
+    assert {l.split()[-1] for l in out.splitlines() if " T " in l} >= _declared()

@@ -1,0 +1,155 @@
+"""GPU tests that need the library's test hooks (forced staging overflows, capacities below the
+defaults, stale sp_set pool generations, a fixed batch-to-context order).  The hooks exist only in
+the test build of the library (lib/libdesamba_test.so, -DDSB_TEST_HOOKS=1; kernels.hip and
+pipeline.c); the production library ignores the same environment variables, which
+test_production_library_ignores_test_hooks checks.  Each scenario runs in a process of its own
+(tests/hook_worker.py) so that the library and its environment are chosen before it loads.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT, golden
+from samutil import groups
+
+pytestmark = pytest.mark.gpu
+
+TEST_LIB = os.path.join(ROOT, "desamba-so_amd", "lib", "libdesamba_test.so")
+PROD_LIB = os.path.join(ROOT, "desamba-so_amd", "lib", "libdesamba.so")
+WORKER = os.path.join(ROOT, "tests", "hook_worker.py")
+
+
+def run_worker(tmp_path, tag, index, inputs, env, lib=TEST_LIB, mode="text", fmt=1, max_read_l=0):
+    """-> (list of output bytes per input, summary dict) of one hook_worker process."""
+    if not os.path.exists(lib):
+        pytest.fail(f"{lib} not built (make -C desamba-so_amd)")
+    spec = {"index": index, "inputs": [str(p) for p in inputs], "fmt": fmt, "mode": mode,
+            "out": str(tmp_path / f"{tag}.out"), "max_read_l": max_read_l}
+    sp = tmp_path / f"{tag}.json"
+    sp.write_text(json.dumps(spec))
+    e = {k: v for k, v in os.environ.items() if not k.startswith("DSB_")}
+    e.update({"DSB_LIB": lib, "DSB_DEVICE": os.environ.get("DSB_DEVICE", "0")})
+    e.update(env)
+    r = subprocess.run([sys.executable, "-u", WORKER, str(sp)], capture_output=True, env=e, timeout=300)
+    assert r.returncode == 0, (tag, r.returncode, r.stderr.decode()[-2000:])
+    summary = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    summary["stderr"] = r.stderr.decode(errors="replace")
+    outs = [open(f"{spec['out']}.{k}", "rb").read() for k in range(len(inputs))]
+    return outs, summary
+
+
+def _golden_files(tmp_path, names):
+    out = []
+    for n in names:
+        p = tmp_path / f"{n}.fq"
+        p.write_bytes(golden(n + ".fq"))
+        out.append(p)
+    return out
+
+
+def test_staging_overflow_replay_is_byte_identical(fixture_index, tmp_path):
+    """DSB_WAVE_DBG=32: two anchors of staging per lane, so every seed group of fast and slow
+    seeding takes the in-order replay path: still byte-identical to the hermetic goldens."""
+    names = ("mixed", "ont", "ont_long")
+    outs, _ = run_worker(tmp_path, "dbg32", fixture_index, _golden_files(tmp_path, names), {"DSB_WAVE_DBG": "32"})
+    for name, out in zip(names, outs):
+        assert out == golden(name + ".herm.sam"), name
+
+
+def test_overflow_reruns_byte_identical(fixture_index, tmp_path):
+    """Every read starts at 1/8 of the default workspace capacities (DSB_TEST_SCALE0=1), so many
+    overflow and are re-run with larger capacities in the retry buffer (several rounds, and with
+    a small budget several chunks): still byte-identical to the hermetic reference."""
+    names = ("mixed", "ont", "ont_long")
+    files = _golden_files(tmp_path, names)
+    for budget in (None, "8"):
+        env = {"DSB_TEST_SCALE0": "1"}
+        if budget:
+            env["DSB_WS_BUDGET_MB"] = budget
+        outs, summ = run_worker(tmp_path, f"scale0_{budget}", fixture_index, files, env)
+        for name, out in zip(names, outs):
+            assert out == golden(name + ".herm.sam"), (name, budget)
+        assert sum(c["n_retry"] for c in summ["calls"]) > 0
+
+
+def test_deferred_reruns_beyond_the_largest_chunk(fixture_index, tmp_path):
+    """Overflow re-runs deferred to the end of a batch (kernels.hip batch_run) from many small
+    chunks: far more deferred reads than any chunk holds, so the re-run's order / carry arrays must
+    be sized for all of them (round-4 advisor finding: they were sized per chunk).  Batch API, every
+    overflowed read deferrable (the run starts from a carry above every read length), byte-identical
+    to the production library's run of the same batch without overflows, with deferral on and off."""
+    fq = tmp_path / "ont_x3.fq"
+    fq.write_bytes(golden("ont.fq") * 3)  # 6000 reads
+    carry = 1 << 20
+    want, _ = run_worker(tmp_path, "prod", fixture_index, [fq], {}, lib=PROD_LIB, mode="batch", max_read_l=carry)
+    for defer in ("1", "0"):
+        env = {"DSB_TEST_SCALE0": "1", "DSB_WS_BUDGET_MB": "16", "DSB_DEFER_RETRY": defer}
+        got, s = run_worker(tmp_path, f"defer{defer}", fixture_index, [fq], env, mode="batch", max_read_l=carry)
+        c = s["calls"][0]
+        print(f"defer {defer}: {c['n_retry']} re-runs over {c['n_chunks']} chunks")
+        assert c["n_retry"] > 1100 and c["n_chunks"] > 50, c
+        assert got[0] == want[0], defer
+
+
+def test_sp_set_pool_sets_never_match_stale_slots(fixture_index, tmp_path):
+    """Regression test for round 3's lost-anchor race, in its round-4 form: the seeding sp_set
+    slots are never cleared; they live in a per-GPU pool of wave-sized sets that seeding waves take
+    and hand back (dsb_kern.h dsb_hpool_acquire / dsb_hpool_release), and a slot matches only the
+    generations of its current holder because every holder moves the set's generation base past the
+    generations it used.  Deterministic form: the same reads X run again and again (X X X X X over
+    two batches, DSB_PIPE_READS = 4 |X|, two contexts sharing one GPU's pool with
+    DSB_GPU_CONTEXTS=2, DSB_TEST_ROUND_ROBIN for the batch-to-context order), so the same reads'
+    seeding waves take sets that waves with the same nodes held before.  Every copy of X must give
+    X's records.  With the base kept in place and sets picked by read length (DSB_WAVE_DBG bit 13,
+    DSB_DBG_POOL_NOGEN), a later copy of a read takes the set an earlier copy filled, meets its
+    slots as live and drops anchors, which this test detects."""
+    lines = golden("ont.fq").split(b"\n")
+    x = b"\n".join(lines[:800]) + b"\n"  # the first 200 four-line records
+    assert x.count(b"\n+\n") == 200
+    fq = tmp_path / "x5.fq"
+    fq.write_bytes(x * 5)
+    env = {"DSB_DEVICES": "0", "DSB_GPU_CONTEXTS": "2", "DSB_PIPE_READS": "800", "DSB_TEST_ROUND_ROBIN": "1"}
+    (out,), s = run_worker(tmp_path, "pool", fixture_index, [fq], env)
+    assert s["devices"] == [0, 0]
+    assert s["calls"][0]["n_batches"] == 2 and s["calls"][0]["n_devices"] == 2
+    g = groups(out)
+    assert len(g) == 1000
+    first = g[:200]
+    for c in range(1, 5):
+        assert g[200 * c:200 * (c + 1)] == first, f"copy {c} of the reads differs"
+    assert first == groups(golden("ont.herm.sam"))[:200]
+    (bad,), _ = run_worker(tmp_path, "pool_nogen", fixture_index, [fq], dict(env, DSB_WAVE_DBG=str(1 << 13)))
+    assert groups(bad) != g, "pool sets handed back without moving their generation base should drop rows: " \
+        "the test would not detect stale slots"
+
+
+def test_production_library_ignores_test_hooks(fixture_index, tmp_path):
+    """The same switches given to the production library change nothing: no forced re-runs, no
+    stale pool generations, the hermetic records."""
+    files = _golden_files(tmp_path, ("ont",))
+    (plain,), s0 = run_worker(tmp_path, "prod_plain", fixture_index, files, {}, lib=PROD_LIB)
+    env = {"DSB_TEST_SCALE0": "1", "DSB_WAVE_DBG": str((1 << 13) | 32), "DSB_WAVE_PHASES": "0"}
+    (out,), s = run_worker(tmp_path, "prod_hooks", fixture_index, files, env, lib=PROD_LIB)
+    assert s["calls"][0]["n_retry"] == s0["calls"][0]["n_retry"]
+    assert out == plain == golden("ont.herm.sam")
+
+
+def test_fenced_pool_hand_over_byte_identical(fixture_index, tmp_path):
+    """The fallback dev_init takes when the XCC ids the device's waves report are not exactly
+    0..n-1 (or the XCC count is unknown): one sp_set pool partition, every hand-over an agent-scope
+    release / acquire.  Forced here (DSB_TEST_POOL_FENCED), two contexts sharing the pool."""
+    names = ("mixed", "ont")
+    env = {"DSB_TEST_POOL_FENCED": "1", "DSB_DEVICES": "0", "DSB_GPU_CONTEXTS": "2", "DSB_PIPE_READS": "300"}
+    outs, s = run_worker(tmp_path, "fenced", fixture_index, _golden_files(tmp_path, names), env)
+    assert "sp_set pool hand-over fenced" in s["stderr"]
+    for name, out in zip(names, outs):
+        assert out == golden(name + ".herm.sam"), name
+
+
+def test_production_pool_is_not_fenced_on_mi355x(fixture_index, tmp_path):
+    """On the MI355X (8 XCDs, ids 0..7) the load-time check passes and the pool runs unfenced."""
+    _, s = run_worker(tmp_path, "unfenced", fixture_index, _golden_files(tmp_path, ("illumina",)), {}, lib=PROD_LIB)
+    assert "hand-over fenced" not in s["stderr"], s["stderr"][-500:]

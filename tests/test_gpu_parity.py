@@ -161,51 +161,6 @@ def test_concurrent_multi_batch_calls_share_contexts_without_deadlock(gpu_index)
     assert serial[0] == golden("mixed.herm.sam_full")
 
 
-def test_sp_set_pool_sets_never_match_stale_slots(pyd, fixture_index):
-    """Regression test for round 3's lost-anchor race, in its round-4 form: the seeding sp_set
-    slots are never cleared; they live in a per-GPU pool of wave-sized sets that seeding waves take
-    and hand back (dsb_kern.h dsb_hpool_acquire / dsb_hpool_release), and a slot matches only the
-    generations of its current holder because every holder moves the set's generation base past the
-    generations it used.  Deterministic form: the same reads X run again and again (X X X X X over
-    two batches, DSB_PIPE_READS = 4 |X|, two contexts sharing one GPU's pool with
-    DSB_GPU_CONTEXTS=2, DSB_TEST_ROUND_ROBIN for the batch-to-context order), so the same reads'
-    seeding waves take sets that waves with the same nodes held before.  Every copy of X must give
-    X's records.  With the base kept in place and sets picked by read length (DSB_WAVE_DBG bit 13,
-    DSB_DBG_POOL_NOGEN), a later copy of a read takes the set an earlier copy filled, meets its
-    slots as live and drops anchors, which this test detects."""
-    lines = golden("ont.fq").split(b"\n")
-    x = b"\n".join(lines[:800]) + b"\n"  # the first 200 four-line records
-    assert x.count(b"\n+\n") == 200
-    data = x * 5
-    env = {"DSB_DEVICES": "0", "DSB_GPU_CONTEXTS": "2", "DSB_PIPE_READS": "800", "DSB_TEST_ROUND_ROBIN": "1"}
-
-    def run(extra):
-        os.environ.update(env)
-        os.environ.update(extra)
-        try:
-            idx = pyd.Index(fixture_index)
-            try:
-                assert idx.devices() == [0, 0]
-                out, t, _ = idx.classify(data, fmt=pyd.FMT_SAM)
-                assert t["n_batches"] == 2 and t["n_devices"] == 2
-                return groups(out)
-            finally:
-                idx.close()
-        finally:
-            for k in list(env) + list(extra):
-                os.environ.pop(k, None)
-
-    g = run({})
-    assert len(g) == 1000
-    first = g[:200]
-    for c in range(1, 5):
-        assert g[200 * c:200 * (c + 1)] == first, f"copy {c} of the reads differs"
-    assert first == groups(golden("ont.herm.sam"))[:200]
-    bad = run({"DSB_WAVE_DBG": str(1 << 13)})
-    assert bad != g, "pool sets handed back without moving their generation base should drop rows: " \
-        "the test would not detect stale slots"
-
-
 def test_two_calls_carry_pool_state_like_one_call(gpu_index, pyd):
     """max_read_l persists per thread_id across read_classify calls (src/cly.c:2953)."""
     fq = golden("mixed.fq")
@@ -374,26 +329,6 @@ def test_many_chunks_and_second_strand_passes_byte_identical(gpu_index, fixture_
         assert fast1 > 0
         print(f"FAST1 MEM searches {fast1}, SLOW1 MEM searches {slow1}")
     finally:
-        os.environ.pop("DSB_WS_BUDGET_MB", None)
-
-
-def test_overflow_reruns_byte_identical(gpu_index, pyd):
-    """Every read starts at 1/8 of the default workspace capacities (DSB_TEST_SCALE0=1), so many
-    overflow and are re-run with larger capacities in the retry buffer (several rounds, and with
-    a small budget several chunks): still byte-identical to the hermetic reference."""
-    os.environ["DSB_TEST_SCALE0"] = "1"
-    try:
-        for budget in (None, "8"):
-            if budget:
-                os.environ["DSB_WS_BUDGET_MB"] = budget
-            retried = 0
-            for name in ("mixed", "ont", "ont_long"):
-                out, t, _ = gpu_index.classify(golden(name + ".fq"), fmt=pyd.FMT_SAM)
-                retried += t["n_retry"]
-                assert out == golden(name + ".herm.sam"), (name, budget)
-            assert retried > 0
-    finally:
-        os.environ.pop("DSB_TEST_SCALE0", None)
         os.environ.pop("DSB_WS_BUDGET_MB", None)
 
 

@@ -12,6 +12,17 @@
 #   suite             the whole -m gpu suite                                            -> suite.log
 #   prof[:ARGS]       rocprofv3 --kernel-trace --stats over bench.py ARGS               -> prof/
 #   pmc:COUNTERS:ARGS one rocprofv3 --pmc pass over bench.py ARGS                        -> pmc_N/
+#                     (tools/traffic_json.py turns a FETCH_SIZE and a WRITE_SIZE pass into
+#                     profiles/traffic.json; tools/prof_report.py pmc DIR prints any pass)
+#   sq[:ARGS]         SQ counters of a 1-step bench.py ARGS (VALU lane utilisation, issue, wait;
+#                     tools/prof_report.py sq)                                          -> sq/
+#   calib[:MB,...]    the random-access calibration (tools/gather_calib.hip: dependent 4-B gathers,
+#                     scattered stores, streams, the read-hash build pattern) with kernel-trace,
+#                     FETCH_SIZE and WRITE_SIZE passes per table size; tools/calib_report.py
+#                                                                                       -> calib/
+#   selftest          the device msort restatement against the host (tools/gpu_selftest.py)
+#   stress[:N]        the committed read sets N times over two contexts, SAM + DES
+#                     (tools/gpu_repeat_sets.py): determinism evidence                   -> stress.txt
 #
 # Usage: gpurun -- 'bash tools/gpu_session.sh r4a bench ab:qcopy,memo:--reads=300000 scale'
 set -o pipefail
@@ -68,6 +79,27 @@ for step in "$@"; do
 		rm -rf "$O/pmc_$npmc"
 		timeout -s KILL 400 rocprofv3 --pmc ${ctr//,/ } -d "$O/pmc_$npmc" -o run -- python3 bench.py ${args:---steps 1 --warmup 0 --no-cpu --no-dropin --no-stats} > "$O/pmc_$npmc.json" 2> "$O/pmc_$npmc.err" || { tail -20 "$O/pmc_$npmc.err"; exit 1; }
 		echo "$ctr" > "$O/pmc_$npmc/counters.txt" ;;
+	sq)
+		rest=${rest//=/ }
+		rm -rf "$O/sq"
+		timeout -s KILL 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD -d "$O/sq" -o sq -- python3 bench.py ${rest:---steps 1 --warmup 0 --no-cpu --no-dropin --no-stats} > "$O/sq.json" 2> "$O/sq.err" || { tail -20 "$O/sq.err"; exit 1; }
+		python3 tools/prof_report.py sq "$O/sq" | tee "$O/sq_util.txt" ;;
+	calib)
+		[ -x tools/gather_calib ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o tools/gather_calib tools/gather_calib.hip || exit 1
+		for mb in ${rest//,/ }; do
+			[ -z "$rest" ] && break
+			timeout -k 10 120 tools/gather_calib $mb 256 > "$O/calib_run_$mb.txt" 2>&1 || exit 1
+			timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$O/calib_kt_$mb" -o kt -- tools/gather_calib $mb 256 > /dev/null 2>&1 || exit 1
+			timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$O/calib_f_$mb" -o f -- tools/gather_calib $mb 256 > /dev/null 2>&1 || exit 1
+			timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$O/calib_w_$mb" -o w -- tools/gather_calib $mb 256 > /dev/null 2>&1 || exit 1
+		done
+		cat "$O"/calib_run_*.txt ;;
+	selftest)
+		timeout -k 10 300 $PY tools/gpu_selftest.py > "$O/selftest.txt" 2>&1 || { tail -20 "$O/selftest.txt"; exit 1; }
+		tail -3 "$O/selftest.txt" ;;
+	stress)
+		timeout -k 10 900 $PY tools/gpu_repeat_sets.py ${rest:-10} > "$O/stress.txt" 2>&1 || { tail -5 "$O/stress.txt"; exit 1; }
+		grep TOTAL_BAD "$O/stress.txt" ;;
 	*)
 		echo "unknown step $step"; exit 2 ;;
 	esac
