@@ -63,6 +63,8 @@ typedef struct dsb_index {
 /* Load deSAMBA.{bwt,sa,exk0,exk1,exki,unv,ref_b,ref_i,ref_p} (idx.c:1103-1160, bwt.c:68-104).
  * Returns 0 on success; on failure writes a message to err. */
 int dsb_index_load_files(dsb_index *ix, const char *dir, char *err, size_t errn);
+/* only the .bwt (occ re-laid out for HBM, rank, and the 13-mer hash index when with_hash) */
+int dsb_index_load_bwt(dsb_index *ix, const char *dir, int with_hash, char *err, size_t errn);
 /* MAPQ tables (cly_mt.c:396-420), P_E 0.15, L_REF = 4 * ref_bin.n */
 void dsb_mapq_tables(dsb_index *ix, double P_E, uint64_t L_REF);
 /* Taxonomy (cly_mt.c:590-670). Returns 0 on success. */

@@ -373,6 +373,20 @@ static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu
 		g->d = share->d;
 		return 0;
 	}
+	{ /* the HBM the tables and the seeding pool take, against what is free: a clear error now
+	   * rather than a failed allocation halfway through the upload */
+		size_t need = ((size_t)ix->n_occ_line + 1) * DSB_OCC_LINE_U64 * 8 + ix->n_occ_super * 32 +
+			      (((size_t)1 << 26) + 1) * 8 + ix->sa_size * 8 + 2 * ix->ek_size + (ix->n_uni + 2) * 8 +
+			      ix->ref_bin_padded + 16 * ix->n_ref + (ix->n_rp + 64) * 8 + 4 * (ix->n_ref + ix->max_tid + 2) +
+			      ((size_t)8 * DSB_HSET_WAVE_U64 + 12) * 8192 * (DSB_HSET_POOL ? 1 : 0) + ((size_t)256 << 20);
+		size_t fr = 0, tot = 0;
+		HIP_OK(hipMemGetInfo(&fr, &tot));
+		if (fr < need) {
+			snprintf(err, errn, "the index needs %.2f GB of HBM on device %d, %.2f GB of %.2f GB are free "
+				 "(another index or another user of the GPU holds the rest)", need / 1e9, device, fr / 1e9, tot / 1e9);
+			return -1;
+		}
+	}
 	dsb_dindex_t &h = g->h;
 	memset(&h, 0, sizeof(h));
 	/* occ lines (128 B per 256 BWT symbols, re-laid out by the loader) + one zero line */
@@ -1291,8 +1305,29 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		size_t ws_want = ws_total + 4096;
 		if (hooks && ws_want > WS.cap)
 			ws_want = std::max(ws_want, std::min((size_t)budget, 2 * WS.cap));
-		if (WS.ensure(ws_want, err, errn) || g->order.ensure(4 * (size_t)cn + 4, err, errn) ||
-		    g->word_off.ensure(8 * (size_t)cn + 16, err, errn))
+		if (WS.ensure(ws_want, err, errn)) {
+			/* HBM short (another index, another user of the GPU, a budget above what is free):
+			 * the exact size, else a chunk of half the bytes, down to one read; never a wait */
+			(void)hipGetLastError();
+			if (ws_want > ws_total + 4096 && WS.ensure(ws_total + 4096, err, errn) == 0) {
+				/* the doubling did not fit; the chunk itself does */
+			} else if (cn > 1) {
+				(void)hipGetLastError();
+				budget = std::max((size_t)1, (size_t)(ws_total / 2));
+				if (hooks)
+					g->pipe_budget = budget;
+				T.n_ws_shrink++;
+				T.n_chunks--;
+				continue; /* re-partition from cb */
+			} else {
+				size_t fr = 0, tot = 0;
+				(void)hipMemGetInfo(&fr, &tot);
+				snprintf(err, errn, "out of HBM: one read of %u bases needs %.1f MB of workspace, %.1f MB free on device %d",
+					 len[cb], ws_total / 1048576.0, fr / 1048576.0, g->device);
+				return -1;
+			}
+		}
+		if (g->order.ensure(4 * (size_t)cn + 4, err, errn) || g->word_off.ensure(8 * (size_t)cn + 16, err, errn))
 			return -1;
 		if (!DSB_HSET_POOL && WS.p != ws_before) /* fresh bytes: no stale sp_set slot may carry a live tag */
 			HIP_OK(hipMemsetAsync(WS.p, 0, WS.cap, s));
@@ -1869,4 +1904,87 @@ extern "C" int dsb_gpu_selftest_sort(uint32_t n, uint32_t n_arrays, int which, u
 			bad++;
 	}
 	return bad;
+}
+
+/* GPU self-test of the occ re-layout on any .bwt, BWTs past 2^32 rows included: for every row,
+ * dsb_occ(r, c) for c = 0..4 and dsb_occ(r, 0xff) with the symbol it reads (7 u64 per row, the
+ * layout of oracle/bigbwt.c occ, which runs the reference's own occ on the same file). */
+__global__ __launch_bounds__(256) void k_selftest_occ(const dsb_dindex_t *__restrict__ ix, const uint64_t *__restrict__ rows,
+							uint64_t n, uint64_t *__restrict__ out)
+{
+	uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	uint64_t r = rows[i];
+	for (int c = 0; c < 5; c++) {
+		uint8_t cc = (uint8_t)c;
+		out[7 * i + c] = dsb_occ(ix, r, &cc);
+	}
+	uint8_t cf = 0xff;
+	out[7 * i + 5] = dsb_occ(ix, r, &cf);
+	out[7 * i + 6] = cf;
+}
+
+extern "C" int dsb_gpu_selftest_occ(const char *dir, uint64_t dollor_pos, const uint64_t *rows, uint64_t n,
+				    uint64_t *out, char *err, size_t errn)
+{
+	dsb_index *ix = (dsb_index *)calloc(1, sizeof(dsb_index));
+	if (!ix) {
+		snprintf(err, errn, "out of memory");
+		return -1;
+	}
+	int rc = -1;
+	if (errn)
+		err[0] = 0;
+	void *d_occ = nullptr, *d_sup = nullptr, *d_rows = nullptr, *d_out = nullptr, *d_ix = nullptr;
+	do {
+		if (dsb_index_load_bwt(ix, dir, 0, err, errn))
+			break;
+		for (uint64_t i = 0; i < n; i++)
+			if (rows[i] >= ix->n_occ_line * DSB_OCC_LINE_SYM) {
+				snprintf(err, errn, "row %lu past the BWT (%lu rows)", (unsigned long)rows[i],
+					 (unsigned long)(ix->n_occ_line * DSB_OCC_LINE_SYM));
+				break;
+			}
+		if (err[0])
+			break;
+		dsb_dindex_t h;
+		memset(&h, 0, sizeof(h));
+		size_t occ_b = (ix->n_occ_line + 1) * DSB_OCC_LINE_U64 * 8, sup_b = ix->n_occ_super * 32;
+		if (hipMalloc(&d_occ, occ_b) != hipSuccess || hipMalloc(&d_sup, sup_b) != hipSuccess ||
+		    hipMalloc(&d_rows, 8 * n + 8) != hipSuccess || hipMalloc(&d_out, 56 * n + 8) != hipSuccess ||
+		    hipMalloc(&d_ix, sizeof(h)) != hipSuccess) {
+			snprintf(err, errn, "hipMalloc failed (%.2f GB of occ lines)", occ_b / 1e9);
+			break;
+		}
+		h.occ = (const uint64_t *)d_occ;
+		h.occ_super = (const uint64_t *)d_sup;
+		h.n_occ_line = ix->n_occ_line;
+		memcpy(h.dollar_row, ix->dollar_row, sizeof(h.dollar_row));
+		h.n_dollar = ix->n_dollar;
+		memcpy(h.rank, ix->rank, sizeof(h.rank));
+		h.dollor_pos = dollor_pos;
+		if (hipMemcpy(d_occ, ix->occ, occ_b, hipMemcpyHostToDevice) != hipSuccess ||
+		    hipMemcpy(d_sup, ix->occ_super, sup_b, hipMemcpyHostToDevice) != hipSuccess ||
+		    hipMemcpy(d_rows, rows, 8 * n, hipMemcpyHostToDevice) != hipSuccess ||
+		    hipMemcpy(d_ix, &h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess) {
+			snprintf(err, errn, "upload failed");
+			break;
+		}
+		if (n)
+			k_selftest_occ<<<(uint32_t)((n + 255) / 256), 256>>>((const dsb_dindex_t *)d_ix, (const uint64_t *)d_rows, n,
+									   (uint64_t *)d_out);
+		if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+		    hipMemcpy(out, d_out, 56 * n, hipMemcpyDeviceToHost) != hipSuccess) {
+			snprintf(err, errn, "occ self-test kernel failed");
+			break;
+		}
+		rc = 0;
+	} while (0);
+	for (void *p : {d_occ, d_sup, d_rows, d_out, d_ix})
+		if (p)
+			(void)hipFree(p);
+	dsb_index_free_host_tables(ix);
+	free(ix);
+	return rc;
 }

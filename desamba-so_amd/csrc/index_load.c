@@ -14,6 +14,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <math.h>
+#include <pthread.h>
 #include "dsb_host.h"
 
 #define REF_BIN_PAD 65536 /* zero bytes after the packed reference (over-reads read 'A') */
@@ -77,10 +78,102 @@ static void set_ekmer_par(dsb_index *ix)
 
 /*
  * occ table re-layout: the reference's 168-B blocks (bwt.c:32-42: u64 count of
- * A,C,G,T,'#' before the block + 256 4-bit symbols) -> one 128-B line per 256 symbols.  The
- * '#' checkpoints the new line drops are re-derived and checked against the file for every
- * block, so the re-layout is verified lossless on each index it loads.
+ * A,C,G,T,'#' before the block + 256 4-bit symbols) -> one 64-B line per 128 symbols + a u64
+ * count table per 2^24-symbol superblock.  Runs in parallel over block ranges: a line's counts come
+ * from its block's checkpoint in the file plus the symbols before it in the block, a superblock's
+ * from the checkpoint of the block it starts at.  The file is verified on the way: every block's
+ * A/C/G/T checkpoints must equal the previous block's plus its symbols, and the '$' count the
+ * '#' checkpoint implies (block start - A - C - G - T - '#') must grow by the '$' symbols of the
+ * block, so the re-layout is lossless on every index it loads (rows are u64 throughout: BWTs past
+ * 2^32 symbols, reference bwt.h:45; tests/test_gpu_bigbwt.py).
  */
+typedef struct {
+	dsb_index *ix;
+	uint64_t b0, b1, nb;          /* blocks [b0, b1) of nb */
+	uint64_t dollar[DSB_MAX_DOLLAR];
+	int n_dollar, bad;
+	char msg[256];
+} relayout_part;
+
+static void *relayout_range(void *arg)
+{
+	relayout_part *P = arg;
+	dsb_index *ix = P->ix;
+	for (uint64_t b = P->b0; b < P->b1 && !P->bad; b++) {
+		const uint8_t *src = ix->bwt_occ + b * 168;
+		uint64_t cnt[5], run[4];
+		memcpy(cnt, src, 40);
+		memcpy(run, cnt, 32);
+		uint64_t dol_before = (b << 8) - cnt[0] - cnt[1] - cnt[2] - cnt[3] - cnt[4], dol = 0;
+		if (b == 0 && (cnt[0] | cnt[1] | cnt[2] | cnt[3] | cnt[4])) {
+			snprintf(P->msg, sizeof(P->msg), "deSAMBA.bwt: block 0 has non-zero checkpoints");
+			P->bad = 1;
+			break;
+		}
+		for (uint32_t k = 0; k < 256; k++) {
+			uint64_t line = (b << 8 | k) / DSB_OCC_LINE_SYM;
+			uint32_t kk = k % DSB_OCC_LINE_SYM;
+			uint64_t *ln = ix->occ + line * DSB_OCC_LINE_U64;
+			if (kk == 0) { /* line start: counts relative to its superblock (which starts at a block) */
+				uint64_t sb_line = line & ~((1ull << DSB_OCC_SUPER_SHIFT) - 1);
+				const uint8_t *sb_src = ix->bwt_occ + (sb_line * DSB_OCC_LINE_SYM / 256) * 168;
+				uint64_t sp[4];
+				memcpy(sp, sb_src, 32);
+				if (line == sb_line)
+					memcpy(ix->occ_super + (line >> DSB_OCC_SUPER_SHIFT) * 4, sp, 32);
+				uint32_t rel[4];
+				for (int c = 0; c < 4; c++)
+					rel[c] = (uint32_t)(run[c] - sp[c]);
+				memcpy(ln, rel, 16);
+			}
+			uint32_t nib = (uint32_t)((src[40 + (k >> 1)] >> ((k & 1) << 2)) & 0xf);
+			if (nib < 4) {
+				ln[2 + (kk >> 5)] |= (uint64_t)nib << (2 * (kk & 31));
+				run[nib]++;
+			} else {
+				ln[6 + (kk >> 6)] |= 1ull << (kk & 63);
+				if (nib == 5) {
+					if (P->n_dollar >= DSB_MAX_DOLLAR) {
+						snprintf(P->msg, sizeof(P->msg), "deSAMBA.bwt: more than %d '$' symbols (unsupported)", DSB_MAX_DOLLAR);
+						P->bad = 1;
+						break;
+					}
+					P->dollar[P->n_dollar++] = (b << 8) + k;
+					dol++;
+				}
+			}
+		}
+		if (b + 1 < P->nb) { /* the next block's checkpoints continue this one's */
+			uint64_t nx[5];
+			memcpy(nx, ix->bwt_occ + (b + 1) * 168, 40);
+			for (int c = 0; c < 4; c++)
+				if (nx[c] != run[c]) {
+					snprintf(P->msg, sizeof(P->msg), "deSAMBA.bwt: block %lu: checkpoint of symbol %d is %lu, %lu counted",
+						 (unsigned long)(b + 1), c, (unsigned long)nx[c], (unsigned long)run[c]);
+					P->bad = 1;
+				}
+			uint64_t nd = ((b + 1) << 8) - nx[0] - nx[1] - nx[2] - nx[3] - nx[4];
+			if (!P->bad && nd != dol_before + dol) {
+				snprintf(P->msg, sizeof(P->msg), "deSAMBA.bwt: block %lu: '#' checkpoint %lu implies %lu '$' before it, %lu counted",
+					 (unsigned long)(b + 1), (unsigned long)nx[4], (unsigned long)nd, (unsigned long)(dol_before + dol));
+				P->bad = 1;
+			}
+		} else { /* the line past the end (occ at r == n) */
+			uint64_t nl = P->nb * (256 / DSB_OCC_LINE_SYM);
+			uint64_t *ln = ix->occ + nl * DSB_OCC_LINE_U64;
+			uint64_t sb_line = nl & ~((1ull << DSB_OCC_SUPER_SHIFT) - 1);
+			uint64_t *sp = ix->occ_super + (nl >> DSB_OCC_SUPER_SHIFT) * 4;
+			if (nl == sb_line)
+				memcpy(sp, run, 32);
+			uint32_t rel[4];
+			for (int c = 0; c < 4; c++)
+				rel[c] = (uint32_t)(run[c] - sp[c]);
+			memcpy(ln, rel, 16);
+		}
+	}
+	return NULL;
+}
+
 static int occ_relayout(dsb_index *ix, char *err, size_t errn)
 {
 	if (ix->byteLen % 168) {
@@ -91,78 +184,67 @@ static int occ_relayout(dsb_index *ix, char *err, size_t errn)
 	uint64_t nb = ix->byteLen / 168;          /* file blocks of 256 symbols */
 	uint64_t nl = nb * (256 / DSB_OCC_LINE_SYM); /* HBM lines */
 	ix->n_occ_line = nl;
-	ix->occ = xm((nl + 1) * DSB_OCC_LINE_U64 * 8); /* + one line past the end (occ at r == n) */
-	memset(ix->occ, 0, (nl + 1) * DSB_OCC_LINE_U64 * 8);
+	ix->occ = calloc((nl + 1) * DSB_OCC_LINE_U64, 8); /* + one line past the end (occ at r == n) */
 	ix->n_occ_super = ((nl + 1) >> DSB_OCC_SUPER_SHIFT) + 1;
-	ix->occ_super = xm(ix->n_occ_super * 4 * 8);
-	memset(ix->occ_super, 0, ix->n_occ_super * 4 * 8);
+	ix->occ_super = calloc(ix->n_occ_super * 4, 8);
+	if (!ix->occ || !ix->occ_super) {
+		snprintf(err, errn, "deSAMBA.bwt: out of host memory for the occ re-layout");
+		return -1;
+	}
 	ix->n_dollar = 0;
-	uint64_t dollars = 0, run[4] = {0, 0, 0, 0};
-	for (uint64_t b = 0; b < nb; b++) {
-		const uint8_t *src = ix->bwt_occ + b * 168;
-		uint64_t cnt[5];
-		memcpy(cnt, src, 40);
-		uint64_t hash_before = (b << 8) - cnt[0] - cnt[1] - cnt[2] - cnt[3] - dollars;
-		if (hash_before != cnt[4]) {
-			snprintf(err, errn, "deSAMBA.bwt: block %lu: '#' checkpoint %lu != %lu derived (unexpected occ layout)",
-				 (unsigned long)b, (unsigned long)cnt[4], (unsigned long)hash_before);
-			return -1;
-		}
-		for (int c = 0; c < 4; c++)
-			if (run[c] != cnt[c]) {
-				snprintf(err, errn, "deSAMBA.bwt: block %lu: checkpoint of symbol %d is %lu, %lu counted",
-					 (unsigned long)b, c, (unsigned long)cnt[c], (unsigned long)run[c]);
-				return -1;
-			}
-		for (uint32_t k = 0; k < 256; k++) {
-			uint64_t line = (b << 8 | k) / DSB_OCC_LINE_SYM;
-			uint32_t kk = k % DSB_OCC_LINE_SYM;
-			uint64_t *ln = ix->occ + line * DSB_OCC_LINE_U64;
-			if (kk == 0) { /* line start: counts relative to the superblock */
-				uint64_t *sp = ix->occ_super + (line >> DSB_OCC_SUPER_SHIFT) * 4;
-				if ((line & ((1ull << DSB_OCC_SUPER_SHIFT) - 1)) == 0)
-					memcpy(sp, run, 32);
-				uint32_t rel[4];
-				for (int c = 0; c < 4; c++)
-					rel[c] = (uint32_t)(run[c] - sp[c]);
-				memcpy(ln, rel, 16);
-			}
-			uint64_t w;
-			memcpy(&w, src + 40 + 8 * (k >> 4), 8);
-			uint32_t nib = (uint32_t)((w >> ((k & 15) << 2)) & 0xf);
-			if (nib < 4) {
-				ln[2 + (kk >> 5)] |= (uint64_t)nib << (2 * (kk & 31));
-				run[nib]++;
-			} else {
-				ln[6 + (kk >> 6)] |= 1ull << (kk & 63);
-				if (nib == 5) {
-					if (ix->n_dollar >= DSB_MAX_DOLLAR) {
-						snprintf(err, errn, "deSAMBA.bwt: more than %d '$' symbols (unsupported)", DSB_MAX_DOLLAR);
-						return -1;
-					}
-					ix->dollar_row[ix->n_dollar++] = (b << 8) + k;
-					dollars++;
-				}
-			}
-		}
+	if (nb == 0)
+		return 0;
+	/* whole superblocks per thread (2^16 blocks): the threads write disjoint lines */
+	const uint64_t sb_blocks = (1ull << DSB_OCC_SUPER_SHIFT) * DSB_OCC_LINE_SYM / 256;
+	uint64_t n_sb = (nb + sb_blocks - 1) / sb_blocks;
+	int nt = dsb_host_threads();
+	if (nt > 64) nt = 64;
+	if ((uint64_t)nt > n_sb) nt = (int)n_sb;
+	if (nt < 1) nt = 1;
+	relayout_part *P = calloc(nt, sizeof(relayout_part));
+	pthread_t *th = calloc(nt, sizeof(pthread_t));
+	for (int t = 0; t < nt; t++) {
+		P[t].ix = ix;
+		P[t].nb = nb;
+		P[t].b0 = n_sb * t / nt * sb_blocks;
+		P[t].b1 = n_sb * (t + 1) / nt * sb_blocks;
+		if (P[t].b1 > nb) P[t].b1 = nb;
 	}
-	{ /* the line past the end */
-		uint64_t *ln = ix->occ + nl * DSB_OCC_LINE_U64;
-		uint64_t *sp = ix->occ_super + (nl >> DSB_OCC_SUPER_SHIFT) * 4;
-		if ((nl & ((1ull << DSB_OCC_SUPER_SHIFT) - 1)) == 0)
-			memcpy(sp, run, 32);
-		uint32_t rel[4];
-		for (int c = 0; c < 4; c++)
-			rel[c] = (uint32_t)(run[c] - sp[c]);
-		memcpy(ln, rel, 16);
+	int started[64] = {0};
+	for (int t = 1; t < nt; t++)
+		started[t] = pthread_create(&th[t], NULL, relayout_range, &P[t]) == 0;
+	relayout_range(&P[0]);
+	for (int t = 1; t < nt; t++) {
+		if (started[t])
+			pthread_join(th[t], NULL);
+		else
+			relayout_range(&P[t]);
 	}
-	return 0;
+	int rc = 0;
+	for (int t = 0; t < nt && !rc; t++)
+		if (P[t].bad) {
+			snprintf(err, errn, "%s", P[t].msg);
+			rc = -1;
+		}
+	for (int t = 0; t < nt && !rc; t++)
+		for (int d = 0; d < P[t].n_dollar; d++) {
+			if (ix->n_dollar >= DSB_MAX_DOLLAR) {
+				snprintf(err, errn, "deSAMBA.bwt: more than %d '$' symbols (unsupported)", DSB_MAX_DOLLAR);
+				rc = -1;
+				break;
+			}
+			ix->dollar_row[ix->n_dollar++] = P[t].dollar[d];
+		}
+	free(P);
+	free(th);
+	return rc;
 }
 
-int dsb_index_load_files(dsb_index *ix, const char *dir, char *err, size_t errn)
+/* .bwt: u64 byteLen | occ blocks | u64 rank[5] | u64 hash_index[2^26+1] (reference load_bwt,
+ * src/bwt.c:68-85), the occ blocks re-laid out for HBM; with_hash 0 skips the 13-mer table */
+int dsb_index_load_bwt(dsb_index *ix, const char *dir, int with_hash, char *err, size_t errn)
 {
 	FILE *f;
-	/* ---- .bwt: u64 byteLen | occ blocks | u64 rank[5] | u64 hash_index[2^26+1] */
 	if (!(f = open_ix(dir, ".bwt", err, errn))) return -1;
 	if (rd(f, &ix->byteLen, 8, 1, "bwt len", err, errn)) goto fail;
 	ix->bwt_occ = xm(ix->byteLen + 256); /* slack: occ may touch the u16 after a block */
@@ -173,12 +255,22 @@ int dsb_index_load_files(dsb_index *ix, const char *dir, char *err, size_t errn)
 	if (occ_relayout(ix, err, errn)) goto fail;
 	free(ix->bwt_occ);
 	ix->bwt_occ = NULL;
-	{
+	if (with_hash) {
 		uint64_t n = (1ull << (DSB_L_PRE_IDX << 1)) + 1;
 		ix->hash_index = xm(n * 8);
 		if (rd(f, ix->hash_index, 8, n, "hash_index", err, errn)) goto fail;
 	}
 	fclose(f);
+	return 0;
+fail:
+	fclose(f);
+	return -1;
+}
+
+int dsb_index_load_files(dsb_index *ix, const char *dir, char *err, size_t errn)
+{
+	FILE *f;
+	if (dsb_index_load_bwt(ix, dir, 1, err, errn)) return -1;
 	/* ---- .sa: u64 n | SA_taxon[n] */
 	if (!(f = open_ix(dir, ".sa", err, errn))) return -1;
 	if (rd(f, &ix->sa_size, 8, 1, "sa n", err, errn)) goto fail;

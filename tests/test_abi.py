@@ -43,7 +43,7 @@ def test_every_declared_function_is_exported(exported):
 
 
 def test_no_undeclared_exports(exported):
-    extra = exported - _declared() - {"dsb_gpu_selftest_sort"}  # self-test hook used by tests/
+    extra = exported - _declared()
     assert not extra, extra
 
 
