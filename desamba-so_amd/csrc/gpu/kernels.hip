@@ -1182,6 +1182,11 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		if (const char *e = getenv("DSB_TEST_SCALE0"))
 			scale0 = (uint32_t)DSB_MAX(1, atoi(e));
 	std::vector<uint32_t> scale(n, scale0);
+	/* DSB_TEST_FORCE_RERUN=k (test build only): every k-th read re-runs as if it had overflowed */
+	uint64_t force_rerun = 0;
+	if (DSB_TEST_HOOKS)
+		if (const char *e = getenv("DSB_TEST_FORCE_RERUN"))
+			force_rerun = strtoull(e, NULL, 10);
 	std::vector<uint64_t> ws_off(n);
 	std::vector<dsb_read_out_t> h_ro(n);
 	std::vector<int32_t> &mrl = b->carry;
@@ -1384,6 +1389,12 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		uint32_t n_over = 0;
 		HIP_OK(copy_wait_g(g, &n_over, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
 		HIP_OK(copy_wait_g(g, h_ro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
+		if (DSB_TEST_HOOKS && force_rerun) /* tests: every k-th read of the batch takes the re-run path */
+			for (uint32_t i = 0; i < cn; i++)
+				if ((cb + i) % force_rerun == 0 && !h_ro[cb + i].status) {
+					h_ro[cb + i].status = 1;
+					n_over++;
+				}
 		hs_mark(HS_SYNC_A);
 		/* ---- max_read_l carry (src/cly.c:2953): prefix max over reads reaching the update; a
 		 * streamed batch takes its carry-in from the batch before it (possibly on another GPU)

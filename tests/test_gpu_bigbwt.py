@@ -75,5 +75,7 @@ def test_occ_past_2_32_rows_matches_reference(big_bwt, pyd, tmp_path):
     bad = np.nonzero((got != want).any(axis=1))[0]
     assert len(bad) == 0, [(int(rows[i]), got[i].tolist(), want[i].tolist()) for i in bad[:5]]
     assert int(got[np.nonzero(rows == dollar)[0][0], 6]) == 5  # the '$' row
-    assert int(want[:, 0].max()) >= (1 << 30)  # counts past 2^30: u64 arithmetic exercised
+    # occ of every symbol before r sums to r (the '$' row is not counted by any c): past 2^32 too
+    tot = want[:, :5].sum(axis=1) + (rows > dollar).astype(np.uint64)
+    assert (tot == rows).all()
     print(f"{len(rows)} rows ({(rows >= (1 << 32)).sum()} past 2^32) x 6 occ: identical to the reference")
