@@ -104,8 +104,9 @@ typedef struct {
 	dsb_chain_t *hit_tmp;
 	dsb_spd_t *sms; uint32_t n_sms;
 	dsb_spd_t *sms_lds;     /* wave scoring: the first DSB_SMS_LDS sms entries live in LDS */
-	uint64_t *lds_key;      /* wave chaining: anchor sort keys / ids in LDS (DSB_SORT_LDS entries), or 0 */
+	uint64_t *lds_key;      /* wave chaining: anchor sort keys / ids in LDS (lds_n entries each), or 0 */
 	uint32_t *lds_id;
+	uint32_t lds_n;         /* entries of lds_key / lds_id: DSB_SORT_LDS, DSB_SORT_LDS_SLOW for the slow resolves */
 	uint16_t *lds_cand;     /* wave scoring: 64 candidate slots of the register k-mer match (DSB_MATCH_BF), or 0 */
 	uint8_t *lds_q;         /* wave scoring: DSB_QCOPY_BYTES of LDS for a window's read range (DSB_QCOPY), or 0 */
 	uint8_t *lds_hb;        /* wave read-hash build: DSB_HB_LDS lane-id bytes in LDS (key groups of a chunk), or 0 */
@@ -2061,6 +2062,10 @@ DSB_HD void dsb_chain_insert_M2(dsb_read_ws *w, uint32_t ai)
  * (ref_ID, direction, ref_offset).  WAVE: bitonic sort of (key, index) pairs (a total order,
  * so the same permutation as any stable sort), keys/indices staged in hit_tmp. */
 #define DSB_SORT_LDS 512
+/* the slow-mode resolves (RESOLVE_S0/S1: ~2% of the reads, a few with thousands of anchors whose
+ * sorts and chain_insert_M3 DP ran from HBM on one wave, ~64 ms per chunk for one read): sorts
+ * of up to 4096 anchors and DP segments of up to the reference's 1024 anchors in LDS (48 KB) */
+#define DSB_SORT_LDS_SLOW 4096
 template <bool WAVE>
 DSB_HD void dsb_sort_anchors(dsb_read_ws *w)
 {
@@ -2079,7 +2084,7 @@ DSB_HD void dsb_sort_anchors(dsb_read_ws *w)
 	while (N < n) N <<= 1;
 	uint64_t *key = (uint64_t *)w->hit_tmp;
 	uint32_t *id = (uint32_t *)(key + N);
-	if (w->lds_key && N <= DSB_SORT_LDS) { /* small sorts run in LDS */
+	if (w->lds_key && N <= w->lds_n) { /* small sorts run in LDS */
 		key = w->lds_key;
 		id = w->lds_id;
 	}
@@ -2118,9 +2123,8 @@ DSB_HD void dsb_sort_anchors(dsb_read_ws *w)
 	dsb_wsync();
 }
 
-/* chain_insert_M3's DP on LDS copies of a segment of up to this many anchors (wave kernels) */
-#define DSB_M3_LDS 256
-static_assert(4 * DSB_M3_LDS <= DSB_SORT_LDS * 2 && 2 * DSB_M3_LDS <= DSB_SORT_LDS, "M3 LDS staging fits the sort arrays");
+/* chain_insert_M3's DP on LDS copies of a segment of up to lds_n / 2 anchors (wave kernels): four
+ * u32 arrays in the sort keys' 8 * lds_n bytes, two in the ids' 4 * lds_n */
 template <bool WAVE>
 DSB_HDN void dsb_chain_insert_M3(dsb_read_ws *w)
 {
@@ -2156,14 +2160,15 @@ DSB_HDN void dsb_chain_insert_M3(dsb_read_ws *w)
 		int32_t max_anchor = -1;
 		int max_score = 0, anchor_max_score;
 		uint32_t seg = chr_ed - chr_st;
-		if (WAVE && !DSB_SEQ(w, 64) && w->lds_key && seg <= DSB_M3_LDS) {
+		const uint32_t M3N = w->lds_n / 2;
+		if (WAVE && !DSB_SEQ(w, 64) && w->lds_key && seg <= M3N) {
 			/* the segment's DP fields staged in LDS (the sort's key/id arrays are free again):
 			 * read offset, reference offset, mtch_len | score << 16, score_v, pre, flags */
 			uint32_t lane = dsb_lane();
-			uint32_t *Lq = (uint32_t *)w->lds_key, *Lt = Lq + DSB_M3_LDS, *Lms = Lt + DSB_M3_LDS;
-			int32_t *Lsv = (int32_t *)(Lms + DSB_M3_LDS);
+			uint32_t *Lq = (uint32_t *)w->lds_key, *Lt = Lq + M3N, *Lms = Lt + M3N;
+			int32_t *Lsv = (int32_t *)(Lms + M3N);
 			int32_t *Lpre = (int32_t *)w->lds_id;
-			uint32_t *Lfl = (uint32_t *)w->lds_id + DSB_M3_LDS;
+			uint32_t *Lfl = (uint32_t *)w->lds_id + M3N;
 			for (uint32_t k = lane; k < seg; k += DSB_WV) {
 				const dsb_anchor_t *a = A + chr_st + k;
 				Lq[k] = a->index_in_read;
@@ -2405,7 +2410,7 @@ DSB_HD void dsb_sort_chains(dsb_read_ws *w, Cmp cmp)
  * chain_cmp_by_score as a stable sort on a key (the comparator is a total preorder, so glibc's
  * stable merge sort and any stable sort give the same permutation): with_top_anchor first, then
  * score = sum_score + 2 (q_ed - q_st) - 4 indel (int arithmetic of src/cly.c:37-51) descending.
- * WAVE + LDS: bitonic sort of (key, index) pairs over the wave for <= DSB_SORT_LDS chains.
+ * WAVE + LDS: bitonic sort of (key, index) pairs over the wave for <= w->lds_n chains.
  */
 template <bool WAVE>
 DSB_HD void dsb_sort_chains_by_score(dsb_read_ws *w)
@@ -2415,7 +2420,7 @@ DSB_HD void dsb_sort_chains_by_score(dsb_read_ws *w)
 		return;
 	uint32_t N = 1;
 	while (N < n) N <<= 1;
-	if (!WAVE || !w->lds_key || N > DSB_SORT_LDS) {
+	if (!WAVE || !w->lds_key || N > w->lds_n) {
 		dsb_sort_chains(w, [](const dsb_chain_t *a, const dsb_chain_t *b) -> int { return dsb_chain_cmp_by_score(a, b); });
 		return;
 	}

@@ -27,9 +27,10 @@
 #ifndef DSB_MINW_RESOLVE
 #define DSB_MINW_RESOLVE 4
 #endif
+/* the slow resolves hold 48 KB of LDS per wave (DSB_SORT_LDS_SLOW): at most 3 per CU anyway */
 #define DSB_MINW_WAVE(PH) ((PH) == DSB_PH_DELA ? DSB_MINW_DELA : \
 			   ((PH) == DSB_PH_FAST0 || (PH) == DSB_PH_FAST1 || (PH) == DSB_PH_SLOW0 || (PH) == DSB_PH_SLOW1) \
-			   ? DSB_MINW_FAST : DSB_MINW_RESOLVE)
+			   ? DSB_MINW_FAST : ((PH) == DSB_PH_RESOLVE_S0 || (PH) == DSB_PH_RESOLVE_S1) ? 1 : DSB_MINW_RESOLVE)
 #define DSB_WIN_LDS_BYTES ((DSB_WIN_BYTES + 15) & ~15)
 /* The scoring phase's reference windows (sdp_middle ref[2000], sdp_right/left ref[1000]) live in
  * LDS, in the same 4 KB the read-hash build uses for its key-group slots before the first window
@@ -659,10 +660,12 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 			(void)last_gen;
 #endif
 		} else if (ph == DSB_PH_RESOLVE_F || ph == DSB_PH_RESOLVE_S0 || ph == DSB_PH_RESOLVE_S1) {
-			__shared__ uint64_t sort_key[DSB_SORT_LDS];
-			__shared__ uint32_t sort_id[DSB_SORT_LDS];
+			constexpr uint32_t NS = (PH == DSB_PH_RESOLVE_S0 || PH == DSB_PH_RESOLVE_S1) ? DSB_SORT_LDS_SLOW : DSB_SORT_LDS;
+			__shared__ uint64_t sort_key[NS];
+			__shared__ uint32_t sort_id[NS];
 			w.lds_key = sort_key;
 			w.lds_id = sort_id;
+			w.lds_n = NS;
 			dsb_phase<true>(&w, &f, ph);
 		} else if (ph == DSB_PH_DELA) {
 			__shared__ uint64_t dela_lds[DSB_DELA_LDS_BYTES / 8];

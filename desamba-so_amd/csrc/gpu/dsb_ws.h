@@ -102,6 +102,7 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 	w->sms_lds = 0;
 	w->lds_key = 0;
 	w->lds_id = 0;
+	w->lds_n = 0;
 	w->lds_hb = 0;
 	w->lds_cand = 0;
 	w->lds_q = 0;

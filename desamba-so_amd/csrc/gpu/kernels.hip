@@ -1509,7 +1509,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			vlen[k] = len[r];
 			vscale[k] = scale[r];
 			vso[k] = b->seq_off[r];
-			vro[k] = ro[r]; /* part A's result: the overflow flag set */
+			vro[k] = h_ro[r]; /* part A's result: the overflow flag set */
 			vmrl[k] = mrl[r];
 		}
 		/* the order / carry / per-read arrays are sized per chunk elsewhere: m (every chunk's

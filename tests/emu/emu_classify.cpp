@@ -127,12 +127,13 @@ int main(int argc, char **argv)
 						gen_base += dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, gen_base, w.mem, sm_lds2) + 1;
 					} else if (ph == DSB_PH_RESOLVE_F || ph == DSB_PH_RESOLVE_S0 || ph == DSB_PH_RESOLVE_S1) {
 						/* the resolve kernels' LDS sort / M3 staging arrays (garbage between reads) */
-						static uint64_t lds_key[DSB_SORT_LDS];
-						static uint32_t lds_id[DSB_SORT_LDS];
+						static uint64_t lds_key[DSB_SORT_LDS_SLOW];
+						static uint32_t lds_id[DSB_SORT_LDS_SLOW];
 						memset(lds_key, 0x5c, sizeof(lds_key));
 						memset(lds_id, 0x5c, sizeof(lds_id));
 						w.lds_key = lds_key;
 						w.lds_id = lds_id;
+						w.lds_n = ph == DSB_PH_RESOLVE_F ? DSB_SORT_LDS : DSB_SORT_LDS_SLOW; /* as dsb_kern.h */
 						dsb_phase<true>(&w, &f, ph);
 						w.lds_key = 0;
 						w.lds_id = 0;
