@@ -280,3 +280,27 @@ def test_c2_proxy_matches_reference(pyd, c2_dir, tmp_path):
     _check_vs_reference(pyd, d, fq, seed, "C2-proxy")
     fq4 = _sim(d, tmp_path, 600, seed + 1, "c4")
     _check_vs_reference(pyd, d, fq4, seed + 1, "C2-proxy-C4-mix")
+
+
+def test_c2_lek18_proxy_matches_reference(pyd, tmp_path):
+    """The next size class of the reference's builder: tools/simulate.py preset c2l18 (1.86 Gbp,
+    ~1.07 G distinct 31-mers >= 2^33 / 9), built on the box by this repo's desamba_index, so the
+    builder itself picks 1 GB e-kmer tables, l_ek 18 and MASK_33 (reference src/idx.c:966-996) over a
+    ~1.1 G-row BWT (66 occ superblocks) — a real index of that class, not C1's BWT with rebuilt
+    tables.  T1/T2 on every read, T3 bounded, against the reference classifier on 1000 fresh ONT
+    reads."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import proxy_build
+    _need(proxy_build.BUILDER)
+    avail = _host_bytes_available()
+    if avail is not None and avail < (96 << 30):
+        pytest.skip(f"host memory short for the c2l18 build: {avail >> 30} GiB available")
+    d = os.environ.get("DSB_C2L18_DIR") or proxy_build.ensure_proxy("c2l18")
+    with open(os.path.join(d, "deSAMBA.exki"), "rb") as f:
+        assert int.from_bytes(f.read(8), "little") == 1 << 30  # the builder chose l_ek 18 / MASK_33
+    with open(os.path.join(d, "deSAMBA.bwt"), "rb") as f:
+        rows = int.from_bytes(f.read(8), "little") // 168 * 256
+    assert rows >= 954_000_000, rows
+    seed = int(os.environ.get("DSB_TEST_SEED", 7272 + int.from_bytes(os.urandom(2), "little")))
+    fq = _sim(d, tmp_path, 1000, seed, "ont")
+    _check_vs_reference(pyd, d, fq, seed, "C2-lek18-proxy")

@@ -291,6 +291,12 @@ PRESETS = {
     "c2": dict(seed=20240603, n_families=80, copies=4, core_len=1300000, flank_len=120000,
                decoy_len=5000, n_shared=8, shared_len=5000,
                repeat_specs=((300, 2000, 0.01), (150, 12000, 0.005))),
+    # the next e-kmer size class: >= 954.4M distinct 31-mers (2^33 / 9), so the builder picks 1 GB
+    # tables, l_ek 18 and MASK_33 (reference idx.c:966-996); the c2 preset's families x 3.75
+    # (1.86 Gbp, ~1.07 G 31-mers, ~1.1 G BWT rows)
+    "c2l18": dict(seed=20240604, n_families=300, copies=4, core_len=1300000, flank_len=120000,
+                  decoy_len=5000, n_shared=8, shared_len=5000,
+                  repeat_specs=((300, 7500, 0.01), (150, 45000, 0.005))),
 }
 
 
