@@ -80,6 +80,17 @@ def ensure_proxy(preset: str, base: str | None = None, build: bool = True, wait_
     parent = os.path.dirname(d)
     os.makedirs(parent, exist_ok=True)
     work = tempfile.mkdtemp(dir=parent, prefix=f"dsb_{preset}_build_")
+    # a heartbeat while the (silent) simulate / build subprocesses run: the GPU box's runner takes a
+    # command that writes nothing for 3 minutes to be hung
+    import threading
+    stop = threading.Event()
+    t_start = time.time()
+
+    def beat():
+        while not stop.wait(30):
+            _log(f"building the {preset} proxy index: {time.time() - t_start:.0f} s")
+    hb = threading.Thread(target=beat, daemon=True)
+    hb.start()
     try:
         t = time.time()
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "simulate.py"), "reference", "--preset", preset,
@@ -87,6 +98,8 @@ def ensure_proxy(preset: str, base: str | None = None, build: bool = True, wait_
         if r.returncode:
             raise RuntimeError(f"simulate.py reference --preset {preset} failed: {r.stderr[-800:]}")
         t_sim = time.time() - t
+        import resource
+        rss_sim = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss  # KB, the largest child so far
         t = time.time()
         idx = os.path.join(work, "idx")
         r = subprocess.run([BUILDER, "-t", str(max(2, usable_cpus())), os.path.join(work, "kmer.srt"), os.path.join(work, "ref.fa"), idx],
@@ -94,10 +107,12 @@ def ensure_proxy(preset: str, base: str | None = None, build: bool = True, wait_
         if r.returncode:
             raise RuntimeError(f"desamba_index failed ({r.returncode}): {r.stderr[-800:]}")
         t_idx = time.time() - t
+        rss_all = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss
         for f in ("nodes.dmp", "names.dmp", "manifest.json"):
             shutil.copy(os.path.join(work, f), os.path.join(idx, f))
         with open(os.path.join(idx, "build.json"), "w") as f:
             json.dump({"preset": preset, "simulate_s": round(t_sim, 1), "desamba_index_s": round(t_idx, 1),
+                       "max_rss_gb_simulate": round(rss_sim / 2**20, 1), "max_rss_gb_any_step": round(rss_all / 2**20, 1),
                        "builder": "desamba-so_amd/bin/desamba_index"}, f)
         if os.path.exists(d):
             shutil.rmtree(d)
@@ -105,6 +120,7 @@ def ensure_proxy(preset: str, base: str | None = None, build: bool = True, wait_
         open(done, "w").close()
         _log(f"{preset} proxy index built in {t_sim:.0f} s (simulate) + {t_idx:.0f} s (desamba_index) -> {d}")
     finally:
+        stop.set()
         shutil.rmtree(work, ignore_errors=True)
     return d
 
