@@ -192,6 +192,80 @@ void load_reference(const char *path, Ref &r)
 		free(buf);
 }
 
+/* ------------------------------------------------------------------ 0: the k-mer list */
+/* SortedKmer "-": the sorted distinct forward 31-mers of every ACGT run (either case) of the
+ * reference, computed here instead of read from a kmer.srt (the file tools/simulate.py writes, and
+ * what the reference's idx_sort makes from a non-canonical jellyfish count, idx_sort.c:101-204).
+ * Parallel: positions in 1 Mbp tasks, k-mers bucketed by their first four bases (two passes:
+ * count, then place), each bucket sorted and de-duplicated on its own, buckets concatenated. */
+void kmers_from_reference(const Ref &ref, Kmers &km)
+{
+	constexpr uint64_t CHUNK = 1 << 20;
+	constexpr int NB = 256;
+	struct Task { uint32_t seq; uint64_t lo, hi; };
+	std::vector<Task> tasks;
+	for (uint32_t i = 0; i < ref.seqs.size(); i++)
+		for (uint64_t lo = 0; lo < ref.seqs[i].len; lo += CHUNK)
+			tasks.push_back({i, lo, std::min(ref.seqs[i].len, lo + CHUNK)});
+	const uint64_t mask = (1ull << 62) - 1;
+	/* the k-mers starting in [lo, hi) of one sequence: f(value) for each one made of ACGT only */
+	auto each = [&](const Task &t, auto &&f) {
+		const char *b = ref.bases.data() + ref.seqs[t.seq].off;
+		uint64_t len = ref.seqs[t.seq].len, v = 0;
+		int run = 0;
+		uint64_t j0 = t.lo >= 30 ? t.lo - 30 : 0; /* the run of bases before the first start position */
+		for (uint64_t j = j0; j < len && j < t.hi + 30; j++) {
+			uint8_t c = BIT[(uint8_t)b[j]];
+			if (c > 3) {
+				run = 0;
+				continue;
+			}
+			v = ((v << 2) | c) & mask;
+			if (++run >= 31 && j - 30 >= t.lo && j - 30 < t.hi)
+				f(v);
+		}
+	};
+	std::vector<uint64_t> cnt(tasks.size() * NB, 0);
+	par_tasks(tasks.size(), g_threads, [&](uint64_t i) {
+		uint64_t *c = cnt.data() + i * NB;
+		each(tasks[i], [&](uint64_t v) { c[v >> 54]++; });
+	});
+	std::vector<uint64_t> bstart(NB + 1, 0), pos(tasks.size() * NB);
+	{
+		uint64_t o = 0;
+		for (int bk = 0; bk < NB; bk++) {
+			bstart[bk] = o;
+			for (uint64_t i = 0; i < tasks.size(); i++) {
+				pos[i * NB + bk] = o;
+				o += cnt[i * NB + bk];
+			}
+		}
+		bstart[NB] = o;
+	}
+	std::vector<uint64_t>().swap(cnt);
+	std::vector<uint64_t> all(bstart[NB]);
+	par_tasks(tasks.size(), g_threads, [&](uint64_t i) {
+		uint64_t *p = pos.data() + i * NB;
+		each(tasks[i], [&](uint64_t v) { all[p[v >> 54]++] = v; });
+	});
+	std::vector<uint64_t> uniq(NB);
+	par_tasks(NB, g_threads, [&](uint64_t bk) {
+		uint64_t *a = all.data() + bstart[bk], *e = all.data() + bstart[bk + 1];
+		std::sort(a, e);
+		uniq[bk] = (uint64_t)(std::unique(a, e) - a);
+	});
+	uint64_t n = 0;
+	for (int bk = 0; bk < NB; bk++) { /* concatenate the buckets' distinct values in place */
+		if (n != bstart[bk])
+			memmove(all.data() + n, all.data() + bstart[bk], 8 * uniq[bk]);
+		n += uniq[bk];
+	}
+	all.resize(n);
+	all.shrink_to_fit();
+	km.v.swap(all);
+	km.n = n;
+}
+
 /* ------------------------------------------------------------------ 1-2: edges and labels */
 void build_edges(const Ref &ref, Kmers &km, std::vector<uint64_t> &heads, std::vector<uint64_t> &tails)
 {
@@ -989,7 +1063,8 @@ int usage()
 {
 	fprintf(stderr,
 		"Usage: desamba_index [-t threads] <SortedKmer> <Reference> <IndexDir>\n"
-		"  SortedKmer  kmer.srt: [u64 n][n sorted distinct 31-mers] (tools/simulate.py reference)\n"
+		"  SortedKmer  kmer.srt: [u64 n][n sorted distinct 31-mers] (tools/simulate.py reference), or -:\n"
+		"              the distinct forward 31-mers of the reference's ACGT runs, computed here\n"
 		"  Reference   FASTA (plain or gzip), all reference sequences in one file\n"
 		"  IndexDir    output directory (created); the same files as `deSAMBA index`\n");
 	return 1;
@@ -1022,7 +1097,13 @@ int main(int argc, char **argv)
 		die("cannot create ", out.dir.c_str());
 
 	Kmers km;
-	{
+	Ref ref;
+	if (!strcmp(kpath, "-")) { /* the k-mer list from the reference itself */
+		load_reference(rpath, ref);
+		note("reference loaded");
+		kmers_from_reference(ref, km);
+		note("k-mers from the reference");
+	} else {
 		FILE *f = fopen(kpath, "rb");
 		if (!f || fread(&km.n, 8, 1, f) != 1)
 			die("cannot read ", kpath);
@@ -1033,15 +1114,14 @@ int main(int argc, char **argv)
 		for (uint64_t i = 1; i < km.n; i++)
 			if (km.v[i] <= km.v[i - 1])
 				die("k-mer file not sorted / not distinct: ", kpath);
-		km.info.assign(km.n, 0);
-		km.bucket.assign((1ull << (2 * LPRE)) + 2, 0);
-		for (uint64_t i = 0; i < km.n; i++) km.bucket[(km.v[i] >> PRE_MOVE) + 1]++;
-		for (uint64_t i = 1; i < km.bucket.size(); i++) km.bucket[i] += km.bucket[i - 1];
+		note("k-mers loaded");
+		load_reference(rpath, ref);
+		note("reference loaded");
 	}
-	note("k-mers loaded");
-	Ref ref;
-	load_reference(rpath, ref);
-	note("reference loaded");
+	km.info.assign(km.n, 0);
+	km.bucket.assign((1ull << (2 * LPRE)) + 2, 0);
+	for (uint64_t i = 0; i < km.n; i++) km.bucket[(km.v[i] >> PRE_MOVE) + 1]++;
+	for (uint64_t i = 1; i < km.bucket.size(); i++) km.bucket[i] += km.bucket[i - 1];
 	std::vector<uint64_t> heads, tails;
 	build_edges(ref, km, heads, tails);
 	note("de Bruijn edges");

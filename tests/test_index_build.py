@@ -115,3 +115,24 @@ def test_missing_kmer_fails_loudly(builder, tmp_path):
     r = subprocess.run([builder, str(tmp_path / "kmer.srt"), str(tmp_path / "ref.fa"), str(tmp_path / "o")],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode != 0 and "missing from the sorted k-mer file" in r.stderr
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_kmer_list_from_the_reference(builder, tmp_path, seed):
+    """SortedKmer "-": the builder computes the distinct forward 31-mers of the reference's ACGT runs
+    itself (parallel, index_build.cpp kmers_from_reference) — the same index as from the k-mer
+    file (lowercase, N / IUPAC breaks and exact 31-base runs included)."""
+    fa, srt = _edge_reference(seed)
+    (tmp_path / "ref.fa").write_bytes(fa)
+    (tmp_path / "kmer.srt").write_bytes(srt)
+    _build(builder, tmp_path / "kmer.srt", tmp_path / "ref.fa", tmp_path / "from_file")
+    r = _build(builder, "-", tmp_path / "ref.fa", tmp_path / "from_ref", {"DSB_HOST_THREADS": "3"})
+    assert "k-mers from the reference" in r.stderr
+    assert "IDENTICAL" in _compare(tmp_path / "from_file", tmp_path / "from_ref")
+
+
+def test_fixture_index_from_reference_kmers(builder, fixture_index, tmp_path):
+    subprocess.run([sys.executable, SIM, "reference", "--preset", "fixture", "--out", str(tmp_path)], check=True,
+                   capture_output=True, timeout=600)
+    _build(builder, "-", tmp_path / "ref.fa", tmp_path / "idx")
+    assert "IDENTICAL" in _compare(fixture_index, tmp_path / "idx")

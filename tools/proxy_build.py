@@ -94,7 +94,7 @@ def ensure_proxy(preset: str, base: str | None = None, build: bool = True, wait_
     try:
         t = time.time()
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "simulate.py"), "reference", "--preset", preset,
-                            "--out", work], capture_output=True, text=True)
+                            "--out", work, "--no-kmers"], capture_output=True, text=True)
         if r.returncode:
             raise RuntimeError(f"simulate.py reference --preset {preset} failed: {r.stderr[-800:]}")
         t_sim = time.time() - t
@@ -102,7 +102,9 @@ def ensure_proxy(preset: str, base: str | None = None, build: bool = True, wait_
         rss_sim = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss  # KB, the largest child so far
         t = time.time()
         idx = os.path.join(work, "idx")
-        r = subprocess.run([BUILDER, "-t", str(max(2, usable_cpus())), os.path.join(work, "kmer.srt"), os.path.join(work, "ref.fa"), idx],
+        # "-": the builder computes the distinct 31-mers of the reference itself (in parallel; the
+        # single-threaded numpy sort of tools/simulate.py's kmer.srt took minutes past 1 Gbp)
+        r = subprocess.run([BUILDER, "-t", str(max(2, usable_cpus())), "-", os.path.join(work, "ref.fa"), idx],
                            capture_output=True, text=True)
         if r.returncode:
             raise RuntimeError(f"desamba_index failed ({r.returncode}): {r.stderr[-800:]}")
@@ -111,7 +113,10 @@ def ensure_proxy(preset: str, base: str | None = None, build: bool = True, wait_
         for f in ("nodes.dmp", "names.dmp", "manifest.json"):
             shutil.copy(os.path.join(work, f), os.path.join(idx, f))
         with open(os.path.join(idx, "build.json"), "w") as f:
-            json.dump({"preset": preset, "simulate_s": round(t_sim, 1), "desamba_index_s": round(t_idx, 1),
+            import re
+            m = re.search(r"\[desamba_index\] (\d+) k-mers, (\d+) unitigs, BWT (\d+) symbols, l_ek (\d+)", r.stderr)
+            counts = dict(zip(("kmers", "unitigs", "bwt_symbols", "l_ek"), map(int, m.groups()))) if m else {}
+            json.dump({"preset": preset, "simulate_s": round(t_sim, 1), "desamba_index_s": round(t_idx, 1), **counts,
                        "max_rss_gb_simulate": round(rss_sim / 2**20, 1), "max_rss_gb_any_step": round(rss_all / 2**20, 1),
                        "builder": "desamba-so_amd/bin/desamba_index"}, f)
         if os.path.exists(d):

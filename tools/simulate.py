@@ -306,6 +306,8 @@ def main(argv=None):
     r = sub.add_parser("reference")
     r.add_argument("--preset", choices=sorted(PRESETS), required=True)
     r.add_argument("--out", required=True, help="output directory")
+    r.add_argument("--no-kmers", action="store_true",
+                   help="skip kmer.srt (desamba_index computes the k-mer list itself when given '-')")
     q = sub.add_parser("reads")
     q.add_argument("--fasta", required=True)
     q.add_argument("--out", required=True)
@@ -322,7 +324,7 @@ def main(argv=None):
         genomes, nodes = make_reference(**p)
         write_fasta(genomes, os.path.join(a.out, "ref.fa"))
         write_taxonomy(nodes, a.out)
-        nk = write_kmer_srt(genomes, os.path.join(a.out, "kmer.srt"))
+        nk = None if a.no_kmers else write_kmer_srt(genomes, os.path.join(a.out, "kmer.srt"))
         meta = dict(preset=a.preset, params={k: (list(v) if isinstance(v, tuple) else v) for k, v in p.items()},
                     n_genomes=len(genomes), total_bp=int(sum(len(g["seq"]) for g in genomes)), n_kmer31=nk)
         with open(os.path.join(a.out, "manifest.json"), "w") as f:
