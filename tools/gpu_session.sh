@@ -54,8 +54,9 @@ for step in "$@"; do
 			elif [[ $v == env.* ]]; then unset DSB_LIB; envs=(); IFS=+ read -ra kvs <<< "${v#env.}"
 				for kv in "${kvs[@]}"; do envs+=("${kv%%.*}=${kv#*.}"); done
 			else export DSB_LIB=desamba-so_amd/lib/var_$v.so; fi
-			env "${envs[@]}" timeout -k 10 300 $PY bench.py --no-cpu --no-stats ${DROPIN---no-dropin} $args > "$O/${name}_$v.json" 2> "$O/${name}_$v.err" || { tail -20 "$O/${name}_$v.err"; exit 1; }
-			python3 -c "import json; d=json.load(open('$O/${name}_$v.json')); print('$v', d['value'], d['ms_per_step'], {k: round(x, 1) for k, x in d['phase_ms_classA'].items()}, 'dropin', (d.get('dropin') or {}).get('value'), (d.get('dropin') or {}).get('identical_to_batch_records'))" | tee -a "$O/$name.txt"
+			vn=${v//\//_} # a file name
+			env "${envs[@]}" timeout -k 10 300 $PY bench.py --no-cpu --no-stats ${DROPIN---no-dropin} $args > "$O/${name}_$vn.json" 2> "$O/${name}_$vn.err" || { tail -20 "$O/${name}_$vn.err"; exit 1; }
+			python3 -c "import json; d=json.load(open('$O/${name}_$vn.json')); print('$vn', d['value'], d['ms_per_step'], 'chunks', d['chunks'], 'retry', d['retried_reads'], {k: round(x, 1) for k, x in d['phase_ms_classA'].items()}, 'dropin', (d.get('dropin') or {}).get('value'), (d.get('dropin') or {}).get('identical_to_batch_records'))" | tee -a "$O/$name.txt"
 		done
 		unset DSB_LIB ;;
 	parity)
