@@ -337,43 +337,56 @@ def cpu_baseline(index_dir: str, fq: bytes, n_sample: int, n_sample_t1: int, gpu
     return out
 
 
-def dropin_leg(idx, fq: bytes, n_reads: int, nb: int, batch_sam_full_sha: str | None):
-    """One read_classify call over the whole batch (reference desamba.h:23): FASTQ text in host
-    memory -> SAM_FULL text in host memory, the index preloaded; the output is checked against
-    the batch path's records for the same reads."""
+def digest(buf) -> str:
+    """Content hash for the drop-in identity check: xxh3-128 (GB/s, the 1M-read SAM_FULL is ~16 GB)
+    when the xxhash module is importable, else sha256."""
+    try:
+        import xxhash
+        return "xxh3_128:" + xxhash.xxh3_128(buf).hexdigest()
+    except ImportError:
+        return "sha256:" + hashlib.sha256(buf).hexdigest()
+
+
+def dropin_leg(idx, fq: bytes, n_reads: int, nb: int, batch_digest: str | None, calls: int = 3):
+    """read_classify over the given reads (reference desamba.h:23): FASTQ text in host memory ->
+    SAM_FULL text in host memory, the index preloaded; the output is checked against the batch
+    path's records for the same reads (content hash, in place)."""
     import ctypes as C
+    import pydesamba as P
     L = idx.L
     out, n = C.c_void_p(), C.c_uint64(0)
     # one untimed call first: the library's pinned staging, device batch buffers and host pool are
     # allocated on first use and kept with the index (a service's steady state)
     L.read_classify(idx.h, fq, len(fq), C.byref(out), C.byref(n), 6, 1)
     L.dsb_free(out)
-    # three timed calls (fresh thread_ids, so each carries its own max_read_l from 0): a single
-    # 0.2-0.3 s call varies by +-10% from run to run; the median is reported, every time kept
-    times, text = [], b""
-    for k in range(3):
+    # timed calls (fresh thread_ids, so each carries its own max_read_l from 0): a single 0.2-0.3 s
+    # call of 100k reads varies by +-10% from run to run; the median is reported, every time kept
+    times, got = [], None
+    for k in range(calls):
         t = time.perf_counter()
         L.read_classify(idx.h, fq, len(fq), C.byref(out), C.byref(n), 7 + k, 1)
         times.append(time.perf_counter() - t)
         if k == 0:
-            text = C.string_at(out.value, n.value) if out.value else b""
+            got = digest(P.view(out.value, n.value) if out.value else b"")
         L.dsb_free(out)
-    secs = sorted(times)[1]
+    secs = sorted(times)[len(times) // 2]
     same = None
-    if batch_sam_full_sha is not None:
-        same = hashlib.sha256(text).hexdigest() == batch_sam_full_sha
-    del text
+    if batch_digest is not None:
+        same = got == batch_digest
     # the same call through dsb_classify_text, for the pipeline's stage times (host wall times)
-    import pydesamba as P
-    _, tm, _ = idx.classify(fq, fmt=P.FMT_SAM_FULL)
+    t = P.Timing()
+    mrl = C.c_int(0)
+    if L.dsb_classify_text(idx.h, fq, len(fq), P.FMT_SAM_FULL, C.byref(mrl), C.byref(out), C.byref(n), C.byref(t)) == 0:
+        L.dsb_free(out)
+    tm = t.as_dict()
     stages = {k: round(tm[k], 2) for k in ("ms_total", "ms_parse", "ms_gather", "ms_format", "ms_wait_gpu", "ms_classA",
                                            "ms_seed", "ms_h2d", "ms_d2h")}
     stages.update({k: int(tm[k]) for k in ("n_batches", "n_devices", "n_view_records", "n_copied_records")})
     return {"value": round(n_reads / secs, 1), "unit": "reads/s", "secs": round(secs, 4),
-            "secs_all": [round(x, 4) for x in times], "value_of": "median of 3 calls",
+            "secs_all": [round(x, 4) for x in times], "value_of": f"median of {calls} calls",
             "gbases_per_s": round(nb / secs / 1e9, 4), "reads": n_reads, "input_bytes": len(fq),
-            "output_bytes": n.value, "identical_to_batch_records": same, "pipeline": stages,
-            "host_threads": int(os.environ.get("DSB_HOST_THREADS", "0")) or None,
+            "output_bytes": n.value, "identical_to_batch_records": same, "check": got.split(":")[0] if got else None,
+            "pipeline": stages, "host_threads": int(os.environ.get("DSB_HOST_THREADS", "0")) or None,
             "what": "read_classify(idx, fastq_text, n, &out, &out_n, 7, 1): parse + H2D + kernels + D2H + "
                     "SAM_FULL formatting, index preloaded"}
 
@@ -427,6 +440,8 @@ def main():
     ap.add_argument("--dropin-reads", type=int, default=100000, help="reads in the end-to-end read_classify leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the end-to-end read_classify leg")
+    ap.add_argument("--dropin-all", type=int, default=1,
+                    help="1: also time one read_classify call over every read of the batch (rank 0, N = 1)")
     ap.add_argument("--no-stats", action="store_true", help="skip the work-counter run (roofline)")
     a = ap.parse_args()
 
@@ -474,7 +489,8 @@ def main():
     log(f"rank {rank}: {batch.n_reads} reads / {batch.n_bases / 1e6:.1f} Mbp resident in HBM "
         f"(parse+upload {batch.upload['ms_h2d']:.0f} ms, {time.time() - t:.1f}s)")
     # the batch holds its own copy of the text: keep only the head the CPU legs use
-    fq = fastq_head(fq, max(a.cpu_sample, a.cpu_sample_t1, a.t3_reads, a.dropin_reads))
+    if not (a.dropin_all and rank == 0 and world == 1 and not a.no_dropin):
+        fq = fastq_head(fq, max(a.cpu_sample, a.cpu_sample_t1, a.t3_reads, a.dropin_reads))
     n_tax = idx.max_tid() + 1
     cdev = "cuda" if (dist is None or dist.get_backend() == "nccl") else "cpu"
     counts = torch.zeros(n_tax, dtype=torch.int64, device=cdev)
@@ -643,15 +659,19 @@ def main():
             cpu = cpu_baseline(index_dir, fq, n_s, min(a.cpu_sample_t1, batch.n_reads),
                                batch.format_range(0, n_s, P.FMT_SAM))
         if not a.no_dropin:
-            full_sha = hashlib.sha256(batch.format_range(0, n_d, P.FMT_SAM_FULL)).hexdigest()
-            dropin = dropin_leg(idx, fq_d, n_d, n_bases(fq_d), full_sha)
+            dropin = dropin_leg(idx, fq_d, n_d, n_bases(fq_d), batch.format_range_hash(0, n_d, P.FMT_SAM_FULL, digest))
+            if a.dropin_all and batch.n_reads > n_d:
+                # the whole batch in one call (the consumer-facing rate at the config's size)
+                dropin["all_reads"] = dropin_leg(idx, fq, batch.n_reads, batch.n_bases,
+                                                 batch.format_range_hash(0, batch.n_reads, P.FMT_SAM_FULL, digest),
+                                                 calls=2)
     elif world > 1 and not a.no_dropin:
         # every rank: one read_classify over its own reads at the same time (after a barrier);
         # aggregate = all ranks' reads / the slowest rank's call
         import pydesamba as P
-        full_sha = hashlib.sha256(batch.format_range(0, n_d, P.FMT_SAM_FULL)).hexdigest()
+        full = batch.format_range_hash(0, n_d, P.FMT_SAM_FULL, digest)
         dist.barrier()
-        mine = dropin_leg(idx, fq_d, n_d, n_bases(fq_d), full_sha)
+        mine = dropin_leg(idx, fq_d, n_d, n_bases(fq_d), full)
         t_s = torch.tensor([mine["secs"]], dtype=torch.float64, device=cdev)
         t_ok = torch.tensor([float(mine["identical_to_batch_records"] is True)], dtype=torch.float64, device=cdev)
         dist.all_reduce(t_s, op=dist.ReduceOp.MAX)

@@ -106,10 +106,16 @@ def lib(path: str | None = None):
     return L
 
 
+def view(ptr: int, n: int) -> memoryview:
+    """The n bytes at ptr, without a copy (ctypes.string_at takes an int size: outputs of 2 GB and
+    more, e.g. SAM_FULL of 1M 8-kb reads, need this)."""
+    return memoryview((C.c_char * n).from_address(ptr)).cast("B") if n else memoryview(b"")
+
+
 def _take(L, p: C.c_void_p, n: int) -> bytes:
     if not p.value:
         return b""
-    b = C.string_at(p.value, n)
+    b = bytes(view(p.value, n))
     L.dsb_free(p)
     return b
 
@@ -214,6 +220,15 @@ class Batch:
         out, n = C.c_void_p(), C.c_uint64(0)
         self.L.dsb_batch_format_range(self.ix.h, self.h, fmt, lo, hi, C.byref(out), C.byref(n))
         return _take(self.L, out, n.value)
+
+    def format_range_hash(self, lo: int, hi: int, fmt: int, fn) -> str:
+        """fn(memoryview) of format_range(lo, hi, fmt), hashed in place (multi-GB outputs)."""
+        out, n = C.c_void_p(), C.c_uint64(0)
+        self.L.dsb_batch_format_range(self.ix.h, self.h, fmt, lo, hi, C.byref(out), C.byref(n))
+        h = fn(view(out.value, n.value) if out.value else b"")
+        if out.value:
+            self.L.dsb_free(out)
+        return h
 
     def carry(self):
         """-> int32[n]: the max_read_l each read's length filter used in the last run."""
