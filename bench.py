@@ -94,6 +94,9 @@ def _tmp():
 WORKLOADS = {
     "c1": ("C1-proxy-56Mbp", os.path.join(ROOT, "data", "c1_index.txz")),
     "c2": ("C2-proxy-495Mbp-lek17", os.path.join(ROOT, "data", "c2_index.txz")),
+    # larger proxies, always built in the run (tools/proxy_build.py): the next e-kmer size classes
+    "c2l18": ("C2-proxy-1.86Gbp-lek18", None),
+    "c2x": ("C2-proxy-3.4Gbp-lek18-2GB", None),
     "fixture": ("C0-fixture-1Mbp", os.path.join(ROOT, "tests", "golden", "fixture_index.txz")),
 }
 
@@ -101,9 +104,9 @@ WORKLOADS = {
 def unpack_index(rank: int, workload: str = "c2") -> tuple[str, str]:
     """-> (index dir, workload name).  Rank 0 unpacks (or builds the C2 proxy), the others wait."""
     name, src = WORKLOADS[workload]
-    if workload == "c2" and not os.path.exists(src):
+    if workload.startswith("c2") and (src is None or not os.path.exists(src)):
         import proxy_build
-        d = proxy_build.ensure_proxy("c2", build=(rank == 0))
+        d = proxy_build.ensure_proxy(workload, build=(rank == 0))
         return d, name
     if not os.path.exists(src):
         if workload != "c1":

@@ -105,4 +105,7 @@ for step in "$@"; do
 		echo "unknown step $step"; exit 2 ;;
 	esac
 done
+for d in "$TMPDIR"/dsb_*_proxy_*/; do # the proxy indexes built in this call: how long, how much memory
+	[ -f "$d/build.json" ] && { b=$(basename "$d"); cp "$d/build.json" "$O/$b.build.json"; cp "$d/build.log" "$O/$b.build.log" 2>/dev/null; }
+done
 echo "[gpu_session] $(date +%T) done" | tee -a "$O/steps.txt"

@@ -112,6 +112,8 @@ def ensure_proxy(preset: str, base: str | None = None, build: bool = True, wait_
         rss_all = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss
         for f in ("nodes.dmp", "names.dmp", "manifest.json"):
             shutil.copy(os.path.join(work, f), os.path.join(idx, f))
+        with open(os.path.join(idx, "build.log"), "w") as f:  # the builder's stage times
+            f.write(r.stderr)
         with open(os.path.join(idx, "build.json"), "w") as f:
             import re
             m = re.search(r"\[desamba_index\] (\d+) k-mers, (\d+) unitigs, BWT (\d+) symbols, l_ek (\d+)", r.stderr)
