@@ -96,7 +96,7 @@ WORKLOADS = {
     "c2": ("C2-proxy-495Mbp-lek17", os.path.join(ROOT, "data", "c2_index.txz")),
     # larger proxies, always built in the run (tools/proxy_build.py): the next e-kmer size classes
     "c2l18": ("C2-proxy-1.86Gbp-lek18", None),
-    "c2x": ("C2-proxy-3.4Gbp-lek18-2GB", None),
+    "c2xl": ("C2-proxy-5Gbp-lek18-bwt-past-2^32", None),
     "fixture": ("C0-fixture-1Mbp", os.path.join(ROOT, "tests", "golden", "fixture_index.txz")),
 }
 

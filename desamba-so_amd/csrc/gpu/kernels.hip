@@ -1232,18 +1232,31 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			if (rused + tot2 + 4096 > g->wsr.cap) {
 				void *np = nullptr;
 				size_t need = rused + tot2 + (rused + tot2) / 2 + 4096;
-				HIP_OK(hipMalloc(&np, need));
+				if (!rused) /* nothing to keep: the old buffer goes first */
+					g->wsr.release();
+				if (hipMalloc(&np, need) != hipSuccess) {
+					(void)hipGetLastError();
+					need = rused + tot2 + 4096; /* no head room, then */
+					if (hipMalloc(&np, need) != hipSuccess) {
+						(void)hipGetLastError();
+						size_t fr = 0, tot = 0;
+						(void)hipMemGetInfo(&fr, &tot);
+						snprintf(err, errn,
+							 "out of HBM: re-running %zu overflowed reads needs %.1f MB of workspace, %.1f MB free on device %d",
+							 sel.size(), need / 1048576.0, fr / 1048576.0, g->device);
+						return -1;
+					}
+				}
 				if (!DSB_HSET_POOL) /* launch-tagged sp_set tables: no stale tag in fresh bytes */
 					HIP_OK(hipMemsetAsync(np, 0, need, s));
 				if (rused)
 					HIP_OK(hipMemcpyAsync(np, g->wsr.p, rused, hipMemcpyDeviceToDevice, s));
 				HIP_OK(hipStreamSynchronize(s));
 				uint64_t delta = (uint64_t)(uintptr_t)np - (uint64_t)(uintptr_t)g->wsr.p;
-				for (uint32_t i = 0; i < cn; i++) /* earlier retried reads move with the buffer */
+				for (uint32_t i = 0; i < cn && rused; i++) /* earlier retried reads move with the buffer */
 					if (vscale[cb + i] > scale0 && !std::binary_search(sel.begin(), sel.end(), i))
 						vws_off[cb + i] += delta;
-				if (g->wsr.p)
-					hipFree(g->wsr.p);
+				g->wsr.release();
 				g->wsr.p = np;
 				g->wsr.cap = need;
 			}
@@ -1496,15 +1509,49 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			fprintf(stderr, " %s %.1f", hs_name[k], hs[k]);
 		fprintf(stderr, " ms\n");
 	}
-	/* ---- the deferred overflow re-runs of every chunk together, then their part B */
+	/* ---- the deferred overflow re-runs of every chunk together, then their part B; in groups whose
+	 * re-run workspace (DSB_CAP_RETRY x capacities) fits the HBM the chunk workspace leaves free.  A
+	 * repeat-rich reference overflows thousands of reads per call: freeing the chunk workspace (it is
+	 * idle now) is cheaper than a failed call */
 	if (!deferred.empty()) {
-		uint32_t m = (uint32_t)deferred.size();
-		std::vector<uint32_t> vlen(m), vscale(m), vidx(m);
-		std::vector<uint64_t> vws(m, 0), vso(m);
-		std::vector<dsb_read_out_t> vro(m);
-		std::vector<int32_t> vmrl(m);
+		size_t fr = 0, tot = 0;
+		(void)hipMemGetInfo(&fr, &tot);
+		uint64_t need_all = 0;
+		for (uint64_t r : deferred)
+			need_all += dsb_layout(len[r], dsb_default_caps(len[r], scale[r] * DSB_CAP_RETRY)).total;
+		if (need_all + need_all / 2 > fr + g->wsr.cap && !hooks) { /* a streamed batch's other context may use it */
+			WS.release();
+			(void)hipMemGetInfo(&fr, &tot);
+			T.n_ws_shrink++;
+		}
+		uint64_t gcap = std::max<uint64_t>((uint64_t)((fr + g->wsr.cap) * 0.45), 1);
+		if (DSB_TEST_HOOKS && getenv("DSB_TEST_RETRY_GROUP_MB")) /* tests: many small groups */
+			gcap = strtoull(getenv("DSB_TEST_RETRY_GROUP_MB"), NULL, 10) << 20;
+		uint32_t n_groups = 0;
+		std::vector<uint32_t> vlen, vscale, vidx;
+		std::vector<uint64_t> vws, vso;
+		std::vector<dsb_read_out_t> vro;
+		std::vector<int32_t> vmrl;
+		for (size_t g0 = 0; g0 < deferred.size();) {
+		size_t g1 = g0;
+		for (uint64_t acc = 0; g1 < deferred.size(); g1++) {
+			uint64_t r = deferred[g1];
+			uint64_t sz = dsb_layout(len[r], dsb_default_caps(len[r], scale[r] * DSB_CAP_RETRY)).total;
+			if (g1 > g0 && acc + sz > gcap)
+				break;
+			acc += sz;
+		}
+		uint32_t m = (uint32_t)(g1 - g0);
+		const uint64_t *dq = deferred.data() + g0;
+		vlen.assign(m, 0);
+		vscale.assign(m, 0);
+		vidx.assign(m, 0);
+		vws.assign(m, 0);
+		vso.assign(m, 0);
+		vro.resize(m);
+		vmrl.assign(m, 0);
 		for (uint32_t k = 0; k < m; k++) {
-			uint64_t r = deferred[k];
+			uint64_t r = dq[k];
 			vidx[k] = (uint32_t)r;
 			vlen[k] = len[r];
 			vscale[k] = scale[r];
@@ -1524,7 +1571,9 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		HIP_OK(copy_wait_g(g, g->vso.p, vso.data(), 8ull * m, hipMemcpyHostToDevice, s));
 		HIP_OK(copy_wait_g(g, g->vidx.p, vidx.data(), 4ull * m, hipMemcpyHostToDevice, s));
 		uint64_t rused = 0;
-		uint8_t *wsb = WS.as<uint8_t>();
+		/* offsets are relative to a base pointer only: the retry buffer's own when the chunk
+		 * workspace was released */
+		uint8_t *wsb = WS.p ? WS.as<uint8_t>() : (uint8_t *)g->wsr.p;
 		const uint32_t *vcl = g->vlen.as<uint32_t>();
 		if (retry_view(m, 0, vlen, vscale, vws, vro, vcl, g->vso.as<uint64_t>(), wsb, rused, m))
 			return -1;
@@ -1556,10 +1605,16 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		if (nh)
 			HIP_OK(copy_wait_g(g, hv.data() + base, g->hits.p, sizeof(dsb_hit_out_t) * nh, hipMemcpyDeviceToHost, s));
 		for (uint32_t k = 0; k < m; k++) {
-			ro[deferred[k]] = vro[k];
-			ro[deferred[k]].hit_off = base + voff[k];
+			ro[dq[k]] = vro[k];
+			ro[dq[k]].hit_off = base + voff[k];
+		}
+		n_groups++;
+		g0 = g1;
 		}
 		hs_mark(HS_RETRY);
+		if (host_timing())
+			fprintf(stderr, "[dsb host] %zu deferred re-runs in %u groups (%.1f MB each at most)\n", deferred.size(),
+				n_groups, gcap / 1048576.0);
 	}
 	*max_read_l = carry;
 	if (tl_bytes && getenv("DSB_TIMELINE")) {

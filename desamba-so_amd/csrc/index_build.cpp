@@ -682,32 +682,57 @@ void build_bwt_string(const Kmers &km, const Unitigs &u, Bwt &bw)
 }
 
 /* ------------------------------------------------------------------ 6-7: FM index, SA walk */
-/* rank structure: one 64-byte line per 64 rows — three bit planes of the symbol codes and the
- * absolute counts of A C G T # before the line (u32: BWT < 2^32 symbols) */
+/* rank structure: one 48-byte line per 64 rows — three bit planes of the symbol codes and the
+ * counts of A C G T # before the line since the start of its 2^32-row superblock (u32), plus the
+ * absolute counts at every superblock start (u64): BWTs past 2^32 rows (the reference's rows are
+ * uint64_t, src/bwt.h:45) */
 struct RankLine {
 	uint64_t plane[3];
 	uint32_t cnt[5];
 	uint32_t pad;
 };
 static_assert(sizeof(RankLine) == 48, "rank line");
+#ifndef RANK_SB_SHIFT
+#define RANK_SB_SHIFT 32 /* tests build it at 16 too (bin/desamba_index_sb16) */
+#endif
 
 struct Rank {
 	std::vector<RankLine> line;
+	std::vector<uint64_t> sb; /* 5 per 2^32 rows */
 	uint64_t C[5];
 	void build(const uint8_t *code, uint64_t n, const uint64_t *rank)
 	{
-		uint64_t nl = (n + 64) / 64;
+		uint64_t nl = (n + 64) / 64, lines_per_sb = 1ull << (RANK_SB_SHIFT - 6);
 		line.assign(nl, RankLine{});
-		uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
-		for (uint64_t l = 0; l < nl; l++) {
-			RankLine &r = line[l];
-			for (int c = 0; c < 5; c++) r.cnt[c] = cnt[c];
-			for (uint64_t i = l * 64; i < std::min(n, l * 64 + 64); i++) {
-				uint8_t x = code[i];
-				for (int b = 0; b < 3; b++) r.plane[b] |= (uint64_t)((x >> b) & 1) << (i & 63);
-				cnt[x]++;
+		sb.assign(5 * ((nl + lines_per_sb - 1) / lines_per_sb), 0);
+		/* superblocks in parallel: counts per superblock first, then the lines */
+		uint64_t nsb = sb.size() / 5;
+		std::vector<uint64_t> tot(6 * nsb, 0);
+		par_tasks(nsb, g_threads, [&](uint64_t k) {
+			uint64_t lo = k << RANK_SB_SHIFT, hi = std::min(n, (k + 1) << RANK_SB_SHIFT);
+			for (uint64_t i = lo; i < hi; i++) tot[6 * k + code[i]]++;
+		});
+		for (uint64_t k = 1; k < nsb; k++)
+			for (int c = 0; c < 5; c++) sb[5 * k + c] = sb[5 * (k - 1) + c] + tot[6 * (k - 1) + c];
+		par_for(nl, g_threads, [&](uint64_t l0, uint64_t l1, int) {
+			if (l0 >= l1)
+				return;
+			/* counts before line l0 within its superblock */
+			uint64_t sbl = (l0 / lines_per_sb) * lines_per_sb;
+			uint32_t cnt[6] = {0, 0, 0, 0, 0, 0};
+			for (uint64_t i = sbl * 64; i < std::min(n, l0 * 64); i++) cnt[code[i]]++;
+			for (uint64_t l = l0; l < l1; l++) {
+				if (l % lines_per_sb == 0)
+					memset(cnt, 0, sizeof(cnt));
+				RankLine &r = line[l];
+				for (int c = 0; c < 5; c++) r.cnt[c] = cnt[c];
+				for (uint64_t i = l * 64; i < std::min(n, l * 64 + 64); i++) {
+					uint8_t x = code[i];
+					for (int b = 0; b < 3; b++) r.plane[b] |= (uint64_t)((x >> b) & 1) << (i & 63);
+					cnt[x]++;
+				}
 			}
-		}
+		});
 		for (int c = 0; c < 5; c++) C[c] = rank[c];
 	}
 	inline uint8_t sym(uint64_t r) const
@@ -724,7 +749,7 @@ struct Rank {
 		uint64_t m1 = (c & 2) ? l.plane[1] : ~l.plane[1];
 		uint64_t m2 = (c & 4) ? l.plane[2] : ~l.plane[2];
 		uint64_t eq = m0 & m1 & m2 & ((1ull << (r & 63)) - 1);
-		return C[c] + l.cnt[c] + (uint64_t)__builtin_popcountll(eq);
+		return C[c] + sb[5 * (r >> RANK_SB_SHIFT) + c] + l.cnt[c] + (uint64_t)__builtin_popcountll(eq);
 	}
 };
 
@@ -1147,8 +1172,6 @@ int main(int argc, char **argv)
 	std::vector<SaTaxon> sa;
 	std::vector<uint8_t> uni;
 	{
-		if (bw.len >= (1ull << 32))
-			die("BWT of 2^32 symbols or more (u32 rank counts)");
 		Rank rk;
 		rk.build(bw.code.data(), bw.len, fm.rank);
 		note("rank structure");

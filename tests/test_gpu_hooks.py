@@ -95,6 +95,24 @@ def test_deferred_reruns_beyond_the_largest_chunk(fixture_index, tmp_path):
         assert got[0] == want[0], defer
 
 
+def test_deferred_reruns_in_groups(fixture_index, tmp_path):
+    """The deferred re-runs of one call go in groups whose re-run workspace fits the HBM the chunk
+    workspace leaves (kernels.hip batch_run; round 5: a repeat-rich proxy overflowed thousands of
+    reads of a 1M-read call and the single re-run buffer did not fit beside a 220-GB chunk
+    workspace).  Groups of at most 4 MB (DSB_TEST_RETRY_GROUP_MB): hundreds of groups, each with its
+    own part B and hit gather, records byte-identical to the production library's."""
+    fq = tmp_path / "ont_x2.fq"
+    fq.write_bytes(golden("ont.fq") * 2)
+    carry = 1 << 20
+    want, _ = run_worker(tmp_path, "prod", fixture_index, [fq], {}, lib=PROD_LIB, mode="batch", max_read_l=carry)
+    env = {"DSB_TEST_FORCE_RERUN": "3", "DSB_WS_BUDGET_MB": "64", "DSB_DEFER_RETRY": "1",
+           "DSB_TEST_RETRY_GROUP_MB": "4"}
+    got, s = run_worker(tmp_path, "groups", fixture_index, [fq], env, mode="batch", max_read_l=carry)
+    c = s["calls"][0]
+    assert c["n_retry"] >= 1300, c
+    assert got[0] == want[0]
+
+
 def test_sp_set_pool_sets_never_match_stale_slots(fixture_index, tmp_path):
     """Regression test for round 3's lost-anchor race, in its round-4 form: the seeding sp_set
     slots are never cleared; they live in a per-GPU pool of wave-sized sets that seeding waves take

@@ -284,9 +284,9 @@ def test_c2_proxy_matches_reference(pyd, c2_dir, tmp_path):
 
 def test_c2_lek18_proxy_matches_reference(pyd, tmp_path):
     """The next size class of the reference's builder: tools/simulate.py preset c2l18 (1.86 Gbp,
-    ~1.07 G distinct 31-mers >= 2^33 / 9), built on the box by this repo's desamba_index, so the
+    ~1.06 G distinct 31-mers >= 2^33 / 9), built on the box by this repo's desamba_index, so the
     builder itself picks 1 GB e-kmer tables, l_ek 18 and MASK_33 (reference src/idx.c:966-996) over a
-    ~1.1 G-row BWT (66 occ superblocks) — a real index of that class, not C1's BWT with rebuilt
+    1.94 G-row BWT (116 occ superblocks) — a real index of that class, not C1's BWT with rebuilt
     tables.  T1/T2 on every read, T3 bounded, against the reference classifier on 1000 fresh ONT
     reads."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -304,3 +304,29 @@ def test_c2_lek18_proxy_matches_reference(pyd, tmp_path):
     seed = int(os.environ.get("DSB_TEST_SEED", 7272 + int.from_bytes(os.urandom(2), "little")))
     fq = _sim(d, tmp_path, 1000, seed, "ont")
     _check_vs_reference(pyd, d, fq, seed, "C2-lek18-proxy")
+
+
+def test_c2xl_proxy_past_2_32_rows_matches_reference(pyd, tmp_path):
+    """The C2 scale: tools/simulate.py preset c2xl (~5 Gbp, ~2.8 G distinct 31-mers, 2 GB e-kmer
+    tables, l_ek 18) built on the box by desamba_index, whose BWT passes 2^32 rows (~17 GB index):
+    occ superblocks, SA samples, LF steps and the relayout's chain checks past the u32 range, in a
+    real index classified end to end.  T1/T2 on every read, T3 bounded, against the reference
+    classifier on 1000 fresh ONT reads.  Builds in ~9 min with ~110 GB of host memory (skipped
+    below that); DSB_C2XL_DIR names a prebuilt one."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import proxy_build
+    _need(proxy_build.BUILDER)
+    d = os.environ.get("DSB_C2XL_DIR")
+    if not d:
+        avail = _host_bytes_available()
+        if avail is not None and avail < (150 << 30):
+            pytest.skip(f"host memory short for the c2xl build: {avail >> 30} GiB available")
+        if not os.environ.get("DSB_RUN_C2XL"):
+            pytest.skip("set DSB_RUN_C2XL=1 (a ~9-minute build) or DSB_C2XL_DIR")
+        d = proxy_build.ensure_proxy("c2xl")
+    with open(os.path.join(d, "deSAMBA.bwt"), "rb") as f:
+        rows = int.from_bytes(f.read(8), "little") // 168 * 256
+    assert rows > 1 << 32, rows
+    seed = int(os.environ.get("DSB_TEST_SEED", 9191 + int.from_bytes(os.urandom(2), "little")))
+    fq = _sim(d, tmp_path, 1000, seed, "ont")
+    _check_vs_reference(pyd, d, fq, seed, "C2-xl-proxy")

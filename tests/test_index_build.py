@@ -136,3 +136,21 @@ def test_fixture_index_from_reference_kmers(builder, fixture_index, tmp_path):
                    capture_output=True, timeout=600)
     _build(builder, "-", tmp_path / "ref.fa", tmp_path / "idx")
     assert "IDENTICAL" in _compare(fixture_index, tmp_path / "idx")
+
+
+def test_rank_superblocks(builder, fixture_index, tmp_path):
+    """The builder's rank structure counts per 2^32-row superblock (index_build.cpp Rank: BWTs past
+    2^32 rows).  bin/desamba_index_sb16 is the same builder with 2^16-row superblocks: the fixture
+    index (~17 superblocks then) rebuilt byte for byte with both SA walks."""
+    exe = os.path.join(ROOT, "desamba-so_amd", "bin", "desamba_index_sb16")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "desamba-so_amd"), "bin/desamba_index_sb16"],
+                       check=True, timeout=600)
+    subprocess.run([sys.executable, SIM, "reference", "--preset", "fixture", "--out", str(tmp_path)], check=True,
+                   capture_output=True, timeout=600)
+    with open(os.path.join(fixture_index, "deSAMBA.bwt"), "rb") as f:
+        rows = int.from_bytes(f.read(8), "little") // 168 * 256
+    assert rows > 4 << 16, rows
+    for ser in ("0", "1"):
+        _build(exe, tmp_path / "kmer.srt", tmp_path / "ref.fa", tmp_path / f"idx{ser}", {"DSB_INDEX_SERIAL_SA": ser})
+        assert "IDENTICAL" in _compare(fixture_index, tmp_path / f"idx{ser}")

@@ -41,7 +41,7 @@ for step in "$@"; do
 	case $name in
 	bench)
 		rest=${rest//=/ }
-		timeout -k 10 560 $PY bench.py ${rest:---steps 5 --warmup 1} > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
+		timeout -k 10 ${BENCH_TIMEOUT:-560} $PY bench.py ${rest:---steps 5 --warmup 1} > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
 		tail -c 600 "$O/bench.json" ;;
 	ab|abd) # abd: with the drop-in leg
 		[ "$name" = abd ] && DROPIN="" || unset DROPIN
@@ -65,13 +65,16 @@ for step in "$@"; do
 	scale)
 		timeout -k 10 900 $PY -m pytest tests/test_gpu_scale.py -x -v -s ${rest:+-k "$rest"} --timeout 600 --timeout-method thread > "$O/scale.log" 2>&1 || { tail -40 "$O/scale.log"; exit 1; }
 		grep -E "PASSED|FAILED|SKIPPED|T3 mismatches" "$O/scale.log" | tail -20 ;;
+	tests) # tests:FILE,FILE  (paths under tests/)
+		timeout -k 10 600 $PY -u -m pytest ${rest//,/ } -x -v --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 || { tail -40 "$O/tests.log"; exit 1; }
+		grep -E "PASSED|FAILED|SKIPPED|ERROR" "$O/tests.log" | tail -30 ;;
 	suite)
 		timeout -k 10 1000 $PY -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > "$O/suite.log" 2>&1 || { tail -40 "$O/suite.log"; exit 1; }
 		tail -3 "$O/suite.log" ;;
 	prof)
 		rest=${rest//=/ }
 		rm -rf "$O/prof"
-		timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py ${rest:---steps 3 --warmup 1 --no-cpu --no-dropin} > "$O/prof_bench.json" 2> "$O/prof.err" || { tail -20 "$O/prof.err"; exit 1; }
+		timeout -k 10 ${PROF_TIMEOUT:-500} rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py ${rest:---steps 3 --warmup 1 --no-cpu --no-dropin} > "$O/prof_bench.json" 2> "$O/prof.err" || { tail -20 "$O/prof.err"; exit 1; }
 		find "$O/prof" -name "*kernel_stats.csv" | head -1 | xargs -r head -12 ;;
 	pmc)
 		ctr=${rest%%:*}; args=${rest#*:}; [ "$args" = "$rest" ] && args=""

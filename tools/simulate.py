@@ -297,11 +297,12 @@ PRESETS = {
     "c2l18": dict(seed=20240604, n_families=300, copies=4, core_len=1300000, flank_len=120000,
                   decoy_len=5000, n_shared=8, shared_len=5000,
                   repeat_specs=((300, 7500, 0.01), (150, 45000, 0.005))),
-    # >= 1.909 G distinct 31-mers (2^34 / 9): 2 GB e-kmer tables, l_ek 18, MASK_34; ~3.4 Gbp, ~2.1 G
-    # 31-mers, a ~2.2 G-row BWT (an index of ~9 GB)
-    "c2x": dict(seed=20240605, n_families=550, copies=4, core_len=1300000, flank_len=120000,
-                decoy_len=5000, n_shared=8, shared_len=5000,
-                repeat_specs=((300, 14000, 0.01), (150, 80000, 0.005))),
+    # a BWT past 2^32 rows (C2's RefSeq-scale index): the c2l18 preset's families x 2.67 (~5 Gbp,
+    # ~2.8 G distinct 31-mers >= 2^34 / 9, so 2 GB e-kmer tables, l_ek 18, MASK_34; ~75 M unitigs;
+    # BWT rows = unitigs x 31 + 31-mers ~ 5.1 G), an index of ~17 GB
+    "c2xl": dict(seed=20240605, n_families=800, copies=4, core_len=1300000, flank_len=120000,
+                 decoy_len=5000, n_shared=8, shared_len=5000,
+                 repeat_specs=((300, 20000, 0.01), (150, 120000, 0.005))),
 }
 
 
