@@ -128,7 +128,9 @@ def cmd_timeline(a):
     raw = (gzip.open(a.file) if a.file.endswith(".gz") else open(a.file, "rb")).read()
     tl = np.frombuffer(raw, dtype=np.uint64).reshape(len(names), stride, 4)
     L = None
-    if a.reads:
+    if a.reads and a.reads.endswith(".npy"):  # tools/first_call.py DSB_SAVE_LENS
+        L = np.load(a.reads)
+    elif a.reads:
         with open(a.reads, "rb") as f:
             L = np.array([len(line) - 1 for i, line in enumerate(f) if i % 4 == 1])
     t0 = min(int(tl[p][tl[p][:, 0] > 0][:, 0].min()) for p in range(len(names)) if (tl[p][:, 0] > 0).any())
