@@ -112,6 +112,8 @@ typedef struct {
 	uint8_t *lds_hb;        /* wave read-hash build: DSB_HB_LDS lane-id bytes in LDS (key groups of a chunk), or 0 */
 	uint32_t *hh[2], *hn[2]; /* read 9-mer hash per strand: list heads per key, one node per position */
 	dsb_sch_t *sch;         /* 256 + 2*400 */
+	uint16_t *sc_off;       /* the seed_con_hash lists as arrays (wave combine_chain): per key [off, off + 1) */
+	uint16_t *sc_flat;      /* into sc_flat, list order; sc_off[256 + k] the tails while the lists are built */
 	uint8_t *win;           /* DSB_WIN_BYTES: sdp_middle ref[2000] and sdp_right/left ref[1000] windows */
 	dsb_mem_t *mem;         /* 16 MEM results per lane (slow mode) */
 	uint64_t *spset;        /* 500 */
@@ -2565,21 +2567,41 @@ DSB_HD void dsb_fill_pattern(dsb_read_ws *w, uint8_t *ref, int lo, int hi)
 #define DSB_MAX_SMS_OVERLAP 6
 
 /* sc_hash_idx, src/cly.c:1686-1705 */
+#define DSB_SC_OFF_U16 (257 + 256 + 256) /* sc_off: list starts, then the tails and the cursors (scratch) */
+#define DSB_SC_FLAT_U16 (2 * 400)
 DSB_HD void dsb_sc_hash_idx(dsb_read_ws *w)
 {
+	/* the lists as the reference links them (a key's entries in insertion order, each list ending
+	 * in an empty node), appended through a tail per key instead of a walk to the end; and the same
+	 * lists as arrays, sc_flat[sc_off[k] .. sc_off[k + 1]), for the wave's combine_chain */
 	dsb_sch_t *sc = w->sch;
-	for (int k = 0; k < 256; k++) { sc[k].next = 0; sc[k].seed_ID_s_or_e = 0; }
+	uint16_t *off = w->sc_off, *tail = off + 257, *cur = off + 257 + 256, *flat = w->sc_flat;
+	for (int k = 0; k < 256; k++) { sc[k].next = 0; sc[k].seed_ID_s_or_e = 0; tail[k] = (uint16_t)k; cur[k] = 0; }
+	for (uint32_t h = 0; h < w->n_hit; h++) {
+		const dsb_chain_t *c_h = w->hit + h;
+		cur[(c_h->t_st - c_h->q_st) & 0xff]++;
+		cur[(c_h->t_ed - c_h->q_ed) & 0xff]++;
+	}
+	uint32_t acc = 0;
+	for (int k = 0; k < 256; k++) {
+		off[k] = (uint16_t)acc;
+		acc += cur[k];
+		cur[k] = off[k];
+	}
+	off[256] = (uint16_t)acc;
 	int sc_con_index = 256;
 	for (uint32_t h = 0; h < w->n_hit; h++) {
-		dsb_chain_t *c_h = w->hit + h;
+		const dsb_chain_t *c_h = w->hit + h;
 		for (int i = 1; i >= 0; i--) {
 			uint16_t c_key = (uint16_t)(((i == 1) ? (c_h->t_st - c_h->q_st) : (c_h->t_ed - c_h->q_ed)) & 0xff);
-			while (sc[c_key].next != 0)
-				c_key = sc[c_key].next;
+			uint16_t node = tail[c_key];
 			/* seed_ID:15 low bits, s_or_e:1 high bit (gcc bitfield order) */
-			sc[c_key].seed_ID_s_or_e = (uint16_t)(((h + 1) & 0x7fff) | ((uint32_t)i << 15));
-			sc[c_key].next = (uint16_t)sc_con_index;
-			sc[sc_con_index++].next = 0;
+			uint16_t e = (uint16_t)(((h + 1) & 0x7fff) | ((uint32_t)i << 15));
+			sc[node].seed_ID_s_or_e = e;
+			sc[node].next = (uint16_t)sc_con_index;
+			sc[sc_con_index].next = 0;
+			tail[c_key] = (uint16_t)sc_con_index++;
+			flat[cur[c_key]++] = e;
 		}
 	}
 }
@@ -3484,31 +3506,73 @@ DSB_HDN int dsb_sdp_middle(dsb_read_ws *w, int32_t c_a_i, const uint8_t *q_str, 
 	return score - 10000;
 }
 
-/* combine_chain, src/cly.c:1758-1803 */
+/* combine_chain, src/cly.c:1758-1803: the first entry of the key's list (in list order) whose
+ * chain continues chain_ID's at this diagonal is merged into it */
+DSB_HD int dsb_comb_ok(const dsb_chain_t *c_h, const dsb_chain_t *c, uint16_t e, int chain_ID, int dis, int isleft,
+			int c_q_pos)
+{
+	int seed_ID = e & 0x7fff;
+	int s_or_e = e >> 15;
+	int dis_con = isleft ? (int)(c->t_ed - c->q_ed) : (int)(c->t_st - c->q_st);
+	int q_pos_con = (!isleft) ? (int)c->q_st : (int)(c->q_ed - DSB_S_A_KMER_L);
+	return dis == dis_con && c_h != c && isleft != s_or_e && DSB_ABS_U(c_q_pos, q_pos_con) < 8 &&
+	       c_h->ref_ID == c->ref_ID && c_h->direction == c->direction && c->sum_score != 0 && seed_ID - 1 > chain_ID;
+}
+
+DSB_HD void dsb_comb_merge(dsb_chain_t *c_h, dsb_chain_t *c)
+{
+	c_h->sum_score += c->sum_score;
+	c_h->anchor_number += c->anchor_number;
+	c_h->indel += c->indel;
+	c_h->q_st = DSB_MIN(c_h->q_st, c->q_st);
+	c_h->t_st = DSB_MIN(c_h->t_st, c->t_st);
+	c_h->q_ed = DSB_MAX(c_h->q_ed, c->q_ed);
+	c_h->t_ed = DSB_MAX(c_h->t_ed, c->t_ed);
+	c->sum_score = 0;
+	c->t_st = c->t_ed = c->q_st = c->q_ed = 0;
+}
+
+template <bool WAVE>
 DSB_HD int dsb_combine_chain_impl(dsb_read_ws *w, int chain_ID, int dis, int isleft, int c_q_pos, int32_t *combined)
 {
 	uint16_t key = (uint16_t)(dis & 0xff);
 	dsb_chain_t *c_h = w->hit + chain_ID;
+	if (WAVE && !DSB_SEQ(w, 4)) {
+		/* the list as an array: one entry per lane, the lowest matching lane is the first match
+		 * in list order (a repeat-rich read puts hundreds of chains on one key: the walk's
+		 * dependent loads were most of its scoring time) */
+		const dsb_chain_t hd = *c_h;
+		uint32_t b = w->sc_off[key], e = w->sc_off[key + 1];
+		for (uint32_t k0 = b; k0 < e; k0 += DSB_WV) {
+			uint32_t k = k0 + dsb_lane();
+			uint16_t ent = 0;
+			int ok = 0;
+			if (k < e) {
+				ent = w->sc_flat[k];
+				const dsb_chain_t *c = w->hit + (ent & 0x7fff) - 1;
+				ok = dsb_comb_ok(&hd, c, ent, chain_ID, dis, isleft, c_q_pos) && c != c_h;
+			}
+			uint64_t bm = dsb_wballot(ok);
+			if (bm) {
+				int first = (int)__builtin_ctzll(bm);
+				int seed_ID = dsb_wshfl((int)ent, first) & 0x7fff;
+				dsb_wsync();
+				if (dsb_lane() == 0)
+					dsb_comb_merge(c_h, w->hit + seed_ID - 1);
+				dsb_wsync();
+				*combined = seed_ID - 1;
+				return 1;
+			}
+		}
+		return 0;
+	}
 	dsb_sch_t *sc = w->sch;
 	while (sc[key].next != 0) {
-		uint16_t seed_ID = sc[key].seed_ID_s_or_e & 0x7fff;
-		int s_or_e = sc[key].seed_ID_s_or_e >> 15;
-		dsb_chain_t *c = w->hit + seed_ID - 1;
-		int dis_con = isleft ? (int)(c->t_ed - c->q_ed) : (int)(c->t_st - c->q_st);
-		int q_pos_con = (!isleft) ? (int)c->q_st : (int)(c->q_ed - DSB_S_A_KMER_L);
-		if (dis == dis_con && c_h != c && isleft != s_or_e && DSB_ABS_U(c_q_pos, q_pos_con) < 8 &&
-		    c_h->ref_ID == c->ref_ID && c_h->direction == c->direction && c->sum_score != 0 &&
-		    (int)seed_ID - 1 > chain_ID) {
-			c_h->sum_score += c->sum_score;
-			c_h->anchor_number += c->anchor_number;
-			c_h->indel += c->indel;
-			c_h->q_st = DSB_MIN(c_h->q_st, c->q_st);
-			c_h->t_st = DSB_MIN(c_h->t_st, c->t_st);
-			c_h->q_ed = DSB_MAX(c_h->q_ed, c->q_ed);
-			c_h->t_ed = DSB_MAX(c_h->t_ed, c->t_ed);
-			c->sum_score = 0;
-			c->t_st = c->t_ed = c->q_st = c->q_ed = 0;
-			*combined = seed_ID - 1;
+		uint16_t ent = sc[key].seed_ID_s_or_e;
+		dsb_chain_t *c = w->hit + (ent & 0x7fff) - 1;
+		if (dsb_comb_ok(c_h, c, ent, chain_ID, dis, isleft, c_q_pos)) {
+			dsb_comb_merge(c_h, c);
+			*combined = (ent & 0x7fff) - 1;
 			return 1;
 		}
 		key = sc[key].next;
@@ -3516,10 +3580,11 @@ DSB_HD int dsb_combine_chain_impl(dsb_read_ws *w, int chain_ID, int dis, int isl
 	return 0;
 }
 
+template <bool WAVE>
 DSB_HD int dsb_combine_chain(dsb_read_ws *w, int chain_ID, int dis, int isleft, int c_q_pos, int32_t *combined)
 {
 	uint64_t t0 = DSB_T0();
-	int r = dsb_combine_chain_impl(w, chain_ID, dis, isleft, c_q_pos, combined);
+	int r = dsb_combine_chain_impl<WAVE>(w, chain_ID, dis, isleft, c_q_pos, combined);
 	DSB_T1(DSB_ST_T_COMB, t0);
 	return r;
 }
@@ -3651,7 +3716,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 		DSB_T1(DSB_ST_T_DPS, tdp0);
 		c_sms->score = (uint32_t)max_score;
 		if (c_sms->len >= 8 &&
-		    dsb_combine_chain(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 0, (int)c_sms->q_pos, &combined)) {
+		    dsb_combine_chain<WAVE>(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 0, (int)c_sms->q_pos, &combined)) {
 			total_max_score = DSB_MAX(score_ori, max_score) - (int)c_sms->len +
 					  dsb_sdp_middle<WAVE>(w, w->hit[combined].cur, q_str, hslot, key_len);
 			if (w->overflow) return 0;
@@ -3806,7 +3871,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 		}
 		DSB_T1(DSB_ST_T_DPS, tdp0);
 		c_sms->score = (uint32_t)max_score;
-		if (c_sms->len >= 8 && dsb_combine_chain(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 1,
+		if (c_sms->len >= 8 && dsb_combine_chain<WAVE>(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 1,
 							 (int)(c_sms->q_pos + c_sms->len), &combined)) {
 			total_max_score = DSB_MAX(score_ori, max_score) - (int)c_sms->len +
 					  dsb_sdp_middle<WAVE>(w, w->hit[combined].cur, q_str, hslot, key_len);

@@ -67,7 +67,7 @@ DSB_HD dsb_ws_layout dsb_layout(uint32_t L, dsb_caps_t cap)
 	o.sms = p; p = dsb_al(p + sizeof(dsb_spd_t) * (uint64_t)cap.sms);
 	o.kl = (uint32_t)dsb_key_len(L);
 	o.hash = p; p = dsb_al(p + 2ull * (4ull * (1ull << o.kl) + 4ull * L)); /* per strand: heads + nodes */
-	o.sch = p; p = dsb_al(p + sizeof(dsb_sch_t) * (256 + 2 * 400 + 64));
+	o.sch = p; p = dsb_al(p + sizeof(dsb_sch_t) * (256 + 2 * 400 + 64) + 2 * (DSB_SC_OFF_U16 + DSB_SC_FLAT_U16));
 	o.win = p; p = dsb_al(p + DSB_WIN_BYTES);
 	o.mem = p; p = dsb_al(p + sizeof(dsb_mem_t) * 16 * 64); /* 16 MEM results per lane (slow seeding) */
 	o.spset = p; p = dsb_al(p + 8 * 512);
@@ -113,6 +113,8 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 		w->hn[s] = h; h += L;
 	}
 	w->sch = (dsb_sch_t *)(base + o.sch);
+	w->sc_off = (uint16_t *)(w->sch + 256 + 2 * 400 + 64);
+	w->sc_flat = w->sc_off + DSB_SC_OFF_U16;
 	w->win = base + o.win;
 	w->mem = (dsb_mem_t *)(base + o.mem);
 	w->spset = (uint64_t *)(base + o.spset);
