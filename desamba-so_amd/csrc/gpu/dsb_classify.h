@@ -3532,15 +3532,81 @@ DSB_HD void dsb_comb_merge(dsb_chain_t *c_h, dsb_chain_t *c)
 	c->t_st = c->t_ed = c->q_st = c->q_ed = 0;
 }
 
+/* combine_chain's candidates for one side (right or left) of one chain's scoring, in the wave:
+ * the later chains (seed_ID - 1 > chain_ID) on c_h's reference and strand that are still live,
+ * lane k holding the k-th in chain order with the diagonal and read position its list entry is
+ * compared on.  A later chain's coordinates are those it had when the lists were built until it
+ * is merged (then zeroed, and dead here too) or scored itself, so the entries the reference's
+ * walk would accept are exactly the cached ones that match, and the first in list order (insertion
+ * order: by chain) is the lowest lane.  Built at the side's first call; more than a wave of
+ * candidates (n < 0) takes the list scan. */
+typedef struct {
+	int built, n;
+	int32_t dis, qpos, sid;
+} dsb_comb_cache;
+
 template <bool WAVE>
-DSB_HD int dsb_combine_chain_impl(dsb_read_ws *w, int chain_ID, int dis, int isleft, int c_q_pos, int32_t *combined)
+DSB_HD int dsb_combine_chain_impl(dsb_read_ws *w, dsb_comb_cache *cc, int chain_ID, int dis, int isleft, int c_q_pos,
+				  int32_t *combined)
 {
 	uint16_t key = (uint16_t)(dis & 0xff);
 	dsb_chain_t *c_h = w->hit + chain_ID;
+	if (WAVE && !DSB_SEQ(w, 4) && cc) {
+		const uint32_t lane = dsb_lane();
+		if (!cc->built) {
+			cc->built = 1;
+			cc->n = 0;
+			cc->dis = cc->qpos = cc->sid = 0;
+			const uint32_t ref = c_h->ref_ID, dir = c_h->direction;
+			for (uint32_t h0 = (uint32_t)chain_ID + 1; h0 < w->n_hit; h0 += DSB_WV) {
+				uint32_t h = h0 + lane;
+				int ok = 0;
+				int32_t d = 0, q = 0;
+				if (h < w->n_hit) {
+					const dsb_chain_t *c = w->hit + h;
+					ok = c->ref_ID == ref && c->direction == dir && c->sum_score != 0;
+					d = isleft ? (int)(c->t_ed - c->q_ed) : (int)(c->t_st - c->q_st);
+					q = isleft ? (int)(c->q_ed - DSB_S_A_KMER_L) : (int)c->q_st;
+				}
+				uint64_t bm = dsb_wballot(ok);
+				int cnt = __builtin_popcountll(bm);
+				if (cc->n + cnt > DSB_WV) {
+					cc->n = -1;
+					break;
+				}
+				if (cnt) {
+					int k = (int)lane - cc->n; /* this lane's place among the new candidates */
+					int mine = k >= 0 && k < cnt;
+					int src = mine ? (int)dsb_select64(bm, (uint32_t)k) : (int)lane;
+					int d2 = dsb_wshfl_any(d, src), q2 = dsb_wshfl_any(q, src), s2 = dsb_wshfl_any((int)h + 1, src);
+					if (mine) {
+						cc->dis = d2;
+						cc->qpos = q2;
+						cc->sid = s2;
+					}
+					cc->n += cnt;
+				}
+			}
+		}
+		if (cc->n >= 0) {
+			int ok = cc->sid != 0 && cc->dis == dis && DSB_ABS_U(c_q_pos, cc->qpos) < 8;
+			uint64_t bm = dsb_wballot(ok);
+			if (!bm)
+				return 0;
+			int seed_ID = dsb_wshfl(cc->sid, (int)__builtin_ctzll(bm));
+			dsb_wsync();
+			if (lane == 0)
+				dsb_comb_merge(c_h, w->hit + seed_ID - 1);
+			dsb_wsync();
+			if (cc->sid == seed_ID)
+				cc->sid = 0; /* merged: zeroed, never a candidate again */
+			*combined = seed_ID - 1;
+			return 1;
+		}
+	}
 	if (WAVE && !DSB_SEQ(w, 4)) {
 		/* the list as an array: one entry per lane, the lowest matching lane is the first match
-		 * in list order (a repeat-rich read puts hundreds of chains on one key: the walk's
-		 * dependent loads were most of its scoring time) */
+		 * in list order */
 		const dsb_chain_t hd = *c_h;
 		uint32_t b = w->sc_off[key], e = w->sc_off[key + 1];
 		for (uint32_t k0 = b; k0 < e; k0 += DSB_WV) {
@@ -3581,10 +3647,11 @@ DSB_HD int dsb_combine_chain_impl(dsb_read_ws *w, int chain_ID, int dis, int isl
 }
 
 template <bool WAVE>
-DSB_HD int dsb_combine_chain(dsb_read_ws *w, int chain_ID, int dis, int isleft, int c_q_pos, int32_t *combined)
+DSB_HD int dsb_combine_chain(dsb_read_ws *w, dsb_comb_cache *cc, int chain_ID, int dis, int isleft, int c_q_pos,
+			     int32_t *combined)
 {
 	uint64_t t0 = DSB_T0();
-	int r = dsb_combine_chain_impl<WAVE>(w, chain_ID, dis, isleft, c_q_pos, combined);
+	int r = dsb_combine_chain_impl<WAVE>(w, cc, chain_ID, dis, isleft, c_q_pos, combined);
 	DSB_T1(DSB_ST_T_COMB, t0);
 	return r;
 }
@@ -3602,6 +3669,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 	int32_t combined;
 	w->n_sms = 0;
 	uint8_t *ref = w->win + DSB_WIN_RL; /* uint8_t ref[1000] (src/cly.c:2537) */
+	dsb_comb_cache cc = {0, 0, 0, 0, 0};
 	dsb_fill_pattern<WAVE>(w, ref, -64, 1000 + 64); /* ref[-1] is read by sdp_left's back extension */
 	dsb_spd_t *p = dsb_push_sms(w);
 	if (!p) return 0;
@@ -3716,7 +3784,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 		DSB_T1(DSB_ST_T_DPS, tdp0);
 		c_sms->score = (uint32_t)max_score;
 		if (c_sms->len >= 8 &&
-		    dsb_combine_chain<WAVE>(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 0, (int)c_sms->q_pos, &combined)) {
+		    dsb_combine_chain<WAVE>(w, &cc, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 0, (int)c_sms->q_pos, &combined)) {
 			total_max_score = DSB_MAX(score_ori, max_score) - (int)c_sms->len +
 					  dsb_sdp_middle<WAVE>(w, w->hit[combined].cur, q_str, hslot, key_len);
 			if (w->overflow) return 0;
@@ -3759,6 +3827,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 	int32_t combined;
 	w->n_sms = 0;
 	uint8_t *ref = w->win + DSB_WIN_RL; /* uint8_t ref[1000] (src/cly.c:2683) */
+	dsb_comb_cache cc = {0, 0, 0, 0, 0};
 	dsb_fill_pattern<WAVE>(w, ref, -64, 1000 + 64); /* ref[-1] is read by sdp_left's back extension */
 	dsb_spd_t *p = dsb_push_sms(w);
 	if (!p) return 0;
@@ -3871,7 +3940,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 		}
 		DSB_T1(DSB_ST_T_DPS, tdp0);
 		c_sms->score = (uint32_t)max_score;
-		if (c_sms->len >= 8 && dsb_combine_chain<WAVE>(w, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 1,
+		if (c_sms->len >= 8 && dsb_combine_chain<WAVE>(w, &cc, chain_ID, (int)(c_sms->t_pos - c_sms->q_pos), 1,
 							 (int)(c_sms->q_pos + c_sms->len), &combined)) {
 			total_max_score = DSB_MAX(score_ori, max_score) - (int)c_sms->len +
 					  dsb_sdp_middle<WAVE>(w, w->hit[combined].cur, q_str, hslot, key_len);

@@ -61,6 +61,20 @@ DSB_HD uint64_t dsb_wmax64(uint64_t v)
 	return v;
 }
 DSB_HD uint64_t dsb_wballot(int p) { return __ballot(p); }
+/* the lane of the k-th (0-based) set bit of a wave mask m (k < popcount(m)) */
+DSB_HD uint32_t dsb_select64(uint64_t m, uint32_t k)
+{
+	uint32_t pos = 0;
+	for (uint32_t w = 32; w; w >>= 1) {
+		uint32_t c = (uint32_t)__builtin_popcountll(m & ((1ull << w) - 1));
+		if (k >= c) {
+			k -= c;
+			m >>= w;
+			pos += w;
+		}
+	}
+	return pos;
+}
 /* *p = max(*p, v) on workgroup-local memory, from any lane */
 DSB_HD void dsb_lds_max(int32_t *p, int32_t v) { atomicMax(p, v); }
 /* value of lane `src` for a per-lane src (ds_bpermute) */
@@ -130,6 +144,7 @@ DSB_HD uint64_t dsb_wmax64(uint64_t v) { return v; }
 DSB_HD uint64_t dsb_wballot(int p) { return p ? 1 : 0; }
 DSB_HD int dsb_wshfl(int v, int src) { (void)src; return v; }
 DSB_HD int dsb_wshfl_any(int v, int src) { (void)src; return v; }
+DSB_HD uint32_t dsb_select64(uint64_t m, uint32_t k) { (void)m; (void)k; return 0; }
 DSB_HD void dsb_lds_max(int32_t *p, int32_t v) { if (v > *p) *p = v; }
 #endif
 
