@@ -700,7 +700,7 @@ def main():
                        "taxon_reduce": f"all_reduce({dist.get_backend()})" if world > 1 else "none"},
             "gbases_per_s": round(bases_total / elapsed / 1e9, 4),
             "classified_reads": classified,
-            "chunks": tms[0]["n_chunks"], "retried_reads": tms[0]["n_retry"],
+            "chunks": tms[0]["n_chunks"], "retried_reads": tms[0]["n_retry"], "heavy_first_reads": tms[0]["n_heavy"],
             "phase_ms": {k: round(sum(t[k] for t in tms) / a.steps, 2)
                          for k in ("ms_encode", "ms_seed", "ms_classA", "ms_classB", "ms_d2h", "ms_total")},
             "phase_ms_classA": {k: round(v, 2) for k, v in phase_ms.items()},

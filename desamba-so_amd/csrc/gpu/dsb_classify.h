@@ -112,6 +112,8 @@ typedef struct {
 	uint8_t *lds_hb;        /* wave read-hash build: DSB_HB_LDS lane-id bytes in LDS (key groups of a chunk), or 0 */
 	uint32_t *hh[2], *hn[2]; /* read 9-mer hash per strand: list heads per key, one node per position */
 	dsb_sch_t *sch;         /* 256 + 2*400 */
+	dsb_chain_t *spec_ch;   /* speculative scoring of one chain (heavy reads, dsb_kern.h k_heavy_spec): its private */
+	uint64_t *spec_bits;    /* copy, and the bitset of the chains it merged (left live in w->hit); else 0 */
 	uint16_t *sc_off;       /* the seed_con_hash lists as arrays (wave combine_chain): per key [off, off + 1) */
 	uint16_t *sc_flat;      /* into sc_flat, list order; sc_off[256 + k] the tails while the lists are built */
 	uint8_t *win;           /* DSB_WIN_BYTES: sdp_middle ref[2000] and sdp_right/left ref[1000] windows */
@@ -3532,6 +3534,25 @@ DSB_HD void dsb_comb_merge(dsb_chain_t *c_h, dsb_chain_t *c)
 	c->t_st = c->t_ed = c->q_st = c->q_ed = 0;
 }
 
+/* the chain being scored: its private copy while scored speculatively (spec_ch), else w->hit */
+DSB_HD dsb_chain_t *dsb_ch(dsb_read_ws *w, int chain_ID) { return w->spec_ch ? w->spec_ch : w->hit + chain_ID; }
+DSB_HD int dsb_spec_merged(const dsb_read_ws *w, uint32_t c) { return w->spec_bits && ((w->spec_bits[c >> 6] >> (c & 63)) & 1); }
+
+/* a speculative merge: c_h takes c's counts and extent as dsb_comb_merge does, c stays as it is in
+ * w->hit (other chains' speculative runs read it) and is only marked merged */
+DSB_HD void dsb_comb_merge_spec(dsb_read_ws *w, dsb_chain_t *c_h, uint32_t ci)
+{
+	const dsb_chain_t *c = w->hit + ci;
+	c_h->sum_score += c->sum_score;
+	c_h->anchor_number += c->anchor_number;
+	c_h->indel += c->indel;
+	c_h->q_st = DSB_MIN(c_h->q_st, c->q_st);
+	c_h->t_st = DSB_MIN(c_h->t_st, c->t_st);
+	c_h->q_ed = DSB_MAX(c_h->q_ed, c->q_ed);
+	c_h->t_ed = DSB_MAX(c_h->t_ed, c->t_ed);
+	w->spec_bits[ci >> 6] |= 1ull << (ci & 63);
+}
+
 /* combine_chain's candidates for one side (right or left) of one chain's scoring, in the wave:
  * the later chains (seed_ID - 1 > chain_ID) on c_h's reference and strand that are still live,
  * lane k holding the k-th in chain order with the diagonal and read position its list entry is
@@ -3550,7 +3571,7 @@ DSB_HD int dsb_combine_chain_impl(dsb_read_ws *w, dsb_comb_cache *cc, int chain_
 				  int32_t *combined)
 {
 	uint16_t key = (uint16_t)(dis & 0xff);
-	dsb_chain_t *c_h = w->hit + chain_ID;
+	dsb_chain_t *c_h = dsb_ch(w, chain_ID);
 	if (WAVE && !DSB_SEQ(w, 4) && cc) {
 		const uint32_t lane = dsb_lane();
 		if (!cc->built) {
@@ -3595,8 +3616,12 @@ DSB_HD int dsb_combine_chain_impl(dsb_read_ws *w, dsb_comb_cache *cc, int chain_
 				return 0;
 			int seed_ID = dsb_wshfl(cc->sid, (int)__builtin_ctzll(bm));
 			dsb_wsync();
-			if (lane == 0)
-				dsb_comb_merge(c_h, w->hit + seed_ID - 1);
+			if (lane == 0) {
+				if (w->spec_bits)
+					dsb_comb_merge_spec(w, c_h, (uint32_t)seed_ID - 1);
+				else
+					dsb_comb_merge(c_h, w->hit + seed_ID - 1);
+			}
 			dsb_wsync();
 			if (cc->sid == seed_ID)
 				cc->sid = 0; /* merged: zeroed, never a candidate again */
@@ -3616,15 +3641,20 @@ DSB_HD int dsb_combine_chain_impl(dsb_read_ws *w, dsb_comb_cache *cc, int chain_
 			if (k < e) {
 				ent = w->sc_flat[k];
 				const dsb_chain_t *c = w->hit + (ent & 0x7fff) - 1;
-				ok = dsb_comb_ok(&hd, c, ent, chain_ID, dis, isleft, c_q_pos) && c != c_h;
+				ok = dsb_comb_ok(&hd, c, ent, chain_ID, dis, isleft, c_q_pos) && c != c_h &&
+				     !dsb_spec_merged(w, (uint32_t)(ent & 0x7fff) - 1);
 			}
 			uint64_t bm = dsb_wballot(ok);
 			if (bm) {
 				int first = (int)__builtin_ctzll(bm);
 				int seed_ID = dsb_wshfl((int)ent, first) & 0x7fff;
 				dsb_wsync();
-				if (dsb_lane() == 0)
-					dsb_comb_merge(c_h, w->hit + seed_ID - 1);
+				if (dsb_lane() == 0) {
+					if (w->spec_bits)
+						dsb_comb_merge_spec(w, c_h, (uint32_t)seed_ID - 1);
+					else
+						dsb_comb_merge(c_h, w->hit + seed_ID - 1);
+				}
 				dsb_wsync();
 				*combined = seed_ID - 1;
 				return 1;
@@ -3665,7 +3695,7 @@ DSB_HDN int dsb_sdp_right(dsb_read_ws *w, const uint8_t *q_str, int hslot, int k
 	score_ori += 10000;
 	int total_max_score = score_ori;
 	int max_sms_id = 0;
-	dsb_chain_t *c_h = w->hit + chain_ID;
+	dsb_chain_t *c_h = dsb_ch(w, chain_ID);
 	int32_t combined;
 	w->n_sms = 0;
 	uint8_t *ref = w->win + DSB_WIN_RL; /* uint8_t ref[1000] (src/cly.c:2537) */
@@ -3823,7 +3853,7 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 	score_ori += 10000;
 	int total_max_score = score_ori;
 	int max_sms_id = 0;
-	dsb_chain_t *c_h = w->hit + chain_ID;
+	dsb_chain_t *c_h = dsb_ch(w, chain_ID);
 	int32_t combined;
 	w->n_sms = 0;
 	uint8_t *ref = w->win + DSB_WIN_RL; /* uint8_t ref[1000] (src/cly.c:2683) */
@@ -3969,6 +3999,25 @@ DSB_HDN int dsb_sdp_left(dsb_read_ws *w, const uint8_t *q_str, int hslot, int ke
 	return total_max_score - 10000;
 }
 
+/* one iteration of get_score_M2's loop (src/cly.c:2832-2842): chain i's middle, right and left
+ * scores; 0 when the read overflowed */
+template <bool WAVE>
+DSB_HD int dsb_score_chain(dsb_read_ws *w, uint32_t i, uint32_t l_read, int key_len)
+{
+	dsb_chain_t *ch = dsb_ch(w, (int)i);
+	const dsb_sdir_t *csd = (w->sd[0].direction == ch->direction) ? &w->sd[0] : &w->sd[1];
+	int hslot = (ch->direction == DSB_FORWARD) ? 0 : 1;
+	const uint8_t *q_str = w->bin + (csd->strand ? w->L : 0);
+	int score = dsb_sdp_middle<WAVE>(w, ch->cur, q_str, hslot, key_len);
+	if (w->overflow) return 0;
+	score = dsb_sdp_right<WAVE>(w, q_str, hslot, key_len, (int)i, l_read, score);
+	if (w->overflow) return 0;
+	score = dsb_sdp_left<WAVE>(w, q_str, hslot, key_len, (int)i, l_read, score);
+	if (w->overflow) return 0;
+	ch->sum_score = (uint32_t)score;
+	return 1;
+}
+
 /* get_score_M2, src/cly.c:2816-2844 */
 template <bool WAVE>
 DSB_HDN void dsb_get_score(dsb_read_ws *w, uint32_t l_read)
@@ -3982,16 +4031,8 @@ DSB_HDN void dsb_get_score(dsb_read_ws *w, uint32_t l_read)
 	for (uint32_t i = 0; i < w->n_hit; i++) {
 		if (w->hit[i].sum_score == 0)
 			continue;
-		const dsb_sdir_t *csd = (w->sd[0].direction == w->hit[i].direction) ? &w->sd[0] : &w->sd[1];
-		int hslot = (w->hit[i].direction == DSB_FORWARD) ? 0 : 1;
-		const uint8_t *q_str = w->bin + (csd->strand ? w->L : 0);
-		int score = dsb_sdp_middle<WAVE>(w, w->hit[i].cur, q_str, hslot, key_len);
-		if (w->overflow) return;
-		score = dsb_sdp_right<WAVE>(w, q_str, hslot, key_len, (int)i, l_read, score);
-		if (w->overflow) return;
-		score = dsb_sdp_left<WAVE>(w, q_str, hslot, key_len, (int)i, l_read, score);
-		if (w->overflow) return;
-		w->hit[i].sum_score = (uint32_t)score;
+		if (!dsb_score_chain<WAVE>(w, i, l_read, key_len))
+			return;
 	}
 }
 
@@ -4019,26 +4060,41 @@ DSB_HD int dsb_chain_cmp_by_MEM_score(const dsb_chain_t *a, const dsb_chain_t *b
 	return (int)(a->sum_score % 2);
 }
 
-/* delete_small_score_rst, src/cly.c:2878-2952 — part A (up to the max_read_l update) */
-template <bool WAVE>
-DSB_HDN void dsb_delete_small_A(dsb_read_ws *w)
+/* delete_small_score_rst, src/cly.c:2878-2952 — part A (up to the max_read_l update), in three
+ * steps: the chains kept and their seed_con_hash (dsb_dela_prep; 0: no chains), the scores
+ * (dsb_get_score, or the heavy reads' speculative scoring, dsb_kern.h), the merges (dsb_dela_post) */
+DSB_HD int dsb_dela_prep(dsb_read_ws *w)
 {
 	w->reached_update = 0;
 	if (w->n_hit == 0)
-		return;
+		return 0;
 	if (w->n_hit > 200) {
 		uint32_t rst_num = 200;
 		for (; rst_num < w->n_hit && w->hit[rst_num].sum_score > 50; rst_num++);
 		w->n_hit = rst_num;
 	}
 	w->n_hit = DSB_MIN(400u, w->n_hit);
-	uint32_t l_read = w->L;
 	dsb_sc_hash_idx(w);
+	return 1;
+}
+
+DSB_HDN void dsb_dela_post(dsb_read_ws *w);
+
+template <bool WAVE>
+DSB_HDN void dsb_delete_small_A(dsb_read_ws *w)
+{
+	if (!dsb_dela_prep(w))
+		return;
 	uint64_t ta0 = DSB_T0();
-	dsb_get_score<WAVE>(w, l_read);
+	dsb_get_score<WAVE>(w, w->L);
 	DSB_T1(DSB_ST_T_ALL, ta0);
 	if (w->overflow)
 		return;
+	dsb_dela_post(w);
+}
+
+DSB_HDN void dsb_dela_post(dsb_read_ws *w)
+{
 	uint32_t n = w->n_hit;
 	if (n > 1)
 		dsb_sort_chains(w, [](const dsb_chain_t *a, const dsb_chain_t *b) -> int { return dsb_chain_cmp_by_pos(a, b); });

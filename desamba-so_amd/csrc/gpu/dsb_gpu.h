@@ -39,6 +39,7 @@ typedef struct {
 	uint64_t n_launch_phase; /* launches of each part-A phase kernel (1 per chunk, 2 when the halves are pipelined) */
 	uint64_t stats[DSB_N_STATS]; /* work counters DSB_ST_*: [32*ph, 32*ph+32) phase ph, [288,320) k_classB */
 	uint64_t n_ws_shrink;    /* chunks re-partitioned smaller because their workspace did not fit in the free HBM */
+	uint64_t n_heavy;        /* scoring reads launched first as heavy (chains x length, kernels.hip k_split) */
 } dsb_gpu_timing;
 
 /* Upload the index to `device`; -1: the DSB_DEVICES list ("all" or "0,1,..."), else the

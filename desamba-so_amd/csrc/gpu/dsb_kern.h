@@ -588,6 +588,25 @@ static_assert(DSB_SM_G == 64 || DSB_SM_G == 32, "lanes per read of the seeding p
 #define DSB_PH_SEEDING(PH) ((PH) == DSB_PH_FAST0 || (PH) == DSB_PH_FAST1 || (PH) == DSB_PH_SLOW0 || (PH) == DSB_PH_SLOW1)
 #define DSB_PH_LANES(PH) (DSB_PH_SEEDING(PH) ? DSB_SM_G : 64)
 
+/* the scoring phase's LDS: reference windows, the read hash build's slots, the register k-mer
+ * match's candidate slots, a window's read range */
+__device__ __forceinline__ void dsb_dela_lds(dsb_read_ws *w, uint64_t *dela_lds)
+{
+	w->lds_hb = (uint8_t *)dela_lds;
+	if (DSB_WIN_IN_LDS)
+		w->win = (uint8_t *)dela_lds;
+	/* the register k-mer match's candidate slots: past the windows, inside the build's area */
+	static_assert(DSB_WIN_LDS_BYTES <= DSB_DELA_CAND_OFF && DSB_DELA_CAND_OFF + 128 <= DSB_DELA_LDS_BYTES,
+		      "candidate slots must not overlap the windows");
+	w->lds_cand = (uint16_t *)((uint8_t *)dela_lds + DSB_DELA_CAND_OFF);
+	/* a window's read range (DSB_QCOPY): the LDS past the windows */
+	static_assert(!DSB_QCOPY || (DSB_WIN_LDS_BYTES + DSB_QCOPY_BYTES <= DSB_DELA_LDS_BYTES && (DSB_WIN_LDS_BYTES & 7) == 0),
+		      "the read-range copy must fit past the windows");
+	static_assert(!(DSB_MATCH_BF && DSB_QCOPY), "the candidate slots share the read-range copy's LDS");
+	if (DSB_QCOPY)
+		w->lds_q = (uint8_t *)dela_lds + DSB_WIN_LDS_BYTES;
+}
+
 /* One read of a phase of part A with one wavefront per read (dsb_wave.h), or a group of
  * DSB_PH_LANES(PH) lanes per read: fast seeding (FAST0/FAST1), chaining (RESOLVE_*), scoring
  * (DELA).  `live`: the group has a read (the last wave of a launch may hold fewer).  The last
@@ -669,19 +688,7 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 			dsb_phase<true>(&w, &f, ph);
 		} else if (ph == DSB_PH_DELA) {
 			__shared__ uint64_t dela_lds[DSB_DELA_LDS_BYTES / 8];
-			w.lds_hb = (uint8_t *)dela_lds;
-			if (DSB_WIN_IN_LDS)
-				w.win = (uint8_t *)dela_lds;
-			/* the register k-mer match's candidate slots: past the windows, inside the build's area */
-			static_assert(DSB_WIN_LDS_BYTES <= DSB_DELA_CAND_OFF && DSB_DELA_CAND_OFF + 128 <= DSB_DELA_LDS_BYTES,
-				      "candidate slots must not overlap the windows");
-			w.lds_cand = (uint16_t *)((uint8_t *)dela_lds + DSB_DELA_CAND_OFF);
-			/* a window's read range (DSB_QCOPY): the LDS past the windows */
-			static_assert(!DSB_QCOPY || (DSB_WIN_LDS_BYTES + DSB_QCOPY_BYTES <= DSB_DELA_LDS_BYTES && (DSB_WIN_LDS_BYTES & 7) == 0),
-				      "the read-range copy must fit past the windows");
-			static_assert(!(DSB_MATCH_BF && DSB_QCOPY), "the candidate slots share the read-range copy's LDS");
-			if (DSB_QCOPY)
-				w.lds_q = (uint8_t *)dela_lds + DSB_WIN_LDS_BYTES;
+			dsb_dela_lds(&w, dela_lds);
 			dsb_phase<true>(&w, &f, ph);
 		} else
 			dsb_phase<true>(&w, &f, ph);
@@ -759,4 +766,178 @@ __global__ __launch_bounds__(64, DSB_MINW_WAVE(PH)) void k_wave_phase(const dsb_
 typedef void (*dsb_phase_fn)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
 			     const uint32_t *, uint32_t, dsb_read_out_t *, uint32_t *, unsigned long long *, uint32_t,
 			     uint64_t);
+
+/*
+ * The scoring of a heavy read (many chains of a long read: kernels.hip k_split) over several waves.
+ * get_score_M2 (src/cly.c:2816-2844) scores the chains in order, and a chain's scoring can merge a
+ * later chain into itself (combine_chain), which zeroes that chain: a later chain's run depends on
+ * the earlier ones only through which chains are zeroed.  So:
+ *   k_heavy_prep   (a wave per read)   the chains kept and their seed_con_hash (dsb_dela_prep);
+ *   k_heavy_spec   (DSB_HEAVY_W waves per read)  every chain scored on its own as if no earlier
+ *                  chain had merged anything: a private copy of the chain (dsb_read_ws.spec_ch),
+ *                  merged chains only marked (spec_bits), its own sms buffer; w->hit is not written;
+ *   k_heavy_fin    (a wave per read)   the chains in order: a chain zeroed by an accepted merge is
+ *                  skipped (as in the reference); a chain whose speculative run merged only chains
+ *                  that are still live took exactly the reference's path (each combine_chain call
+ *                  accepts the first live match in list order, and the live set it ran against
+ *                  differs from the true one only by chains it did not pick), so its result and
+ *                  merges are applied; any other chain is scored again, in order, by this wave.
+ *                  Then the rest of delete_small_score_rst part A (dsb_dela_post).
+ * Scratch per read (host-laid out, dsb_heavy_bytes): DSB_HEAVY_MAX_HIT records, then a sms buffer
+ * per wave.
+ */
+#define DSB_HEAVY_W 16
+#define DSB_HEAVY_MAX_HIT 400
+/* launch signatures (kernels.hip takes the kernels from the scoring phase's unit, phase.hip) */
+typedef void (*dsb_heavy_prep_fn)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
+				  const uint32_t *, uint32_t, uint32_t);
+typedef void (*dsb_heavy_spec_fn)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
+				  const uint32_t *, uint32_t, uint8_t *, const uint64_t *, uint32_t);
+typedef void (*dsb_heavy_fin_fn)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,
+				 const uint32_t *, uint32_t, uint8_t *, const uint64_t *, dsb_read_out_t *, uint32_t *, uint32_t);
+typedef struct {
+	dsb_chain_t ch;         /* the chain after its speculative run (sum_score = its score) */
+	uint32_t flags;         /* 1 scored, 2 the run overflowed (the finalising wave scores it again) */
+	uint32_t pad;
+	uint64_t bits[(DSB_HEAVY_MAX_HIT + 63) / 64]; /* chains it merged */
+} dsb_heavy_rec;
+DSB_HD uint64_t dsb_heavy_bytes(uint32_t L, uint32_t scale)
+{
+	dsb_caps_t cap = dsb_default_caps(L, scale);
+	return dsb_al(sizeof(dsb_heavy_rec) * DSB_HEAVY_MAX_HIT) + DSB_HEAVY_W * dsb_al(sizeof(dsb_spd_t) * (uint64_t)cap.sms);
+}
+
+__device__ __forceinline__ void dsb_heavy_ws(const dsb_dindex_t *ix, const uint32_t *len, const uint64_t *ws_off,
+					     const uint32_t *scale, uint8_t *ws, uint32_t r, dsb_read_ws *w, dsb_rflags_t *f,
+					     dsb_rstate_t **sp, uint32_t dbg)
+{
+	uint32_t L = len[r];
+	uint8_t *base = ws + ws_off[r];
+	dsb_caps_t cap = dsb_default_caps(L, scale[r]);
+	dsb_ws_layout lay = dsb_layout(L, cap);
+	dsb_ws_init(w, ix, base, L, cap);
+	*sp = (dsb_rstate_t *)(base + lay.state);
+	dsb_state_load(w, f, *sp);
+	w->dbg = dbg;
+}
+
+template <int V>
+__global__ __launch_bounds__(64) void k_heavy_prep(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+						   const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+						   uint8_t *__restrict__ ws, const uint32_t *__restrict__ hl, uint32_t nh, uint32_t dbg)
+{
+	if (blockIdx.x >= nh)
+		return;
+	dsb_read_ws w;
+	dsb_rflags_t f;
+	dsb_rstate_t *sp;
+	dsb_heavy_ws(ix, len, ws_off, scale, ws, hl[blockIdx.x], &w, &f, &sp, dbg);
+	if (threadIdx.x == 0) { /* scalar work, one lane */
+		dsb_dela_prep(&w);
+		dsb_state_save(&w, &f, sp);
+	}
+}
+
+template <int V>
+__global__ __launch_bounds__(64, 4) void k_heavy_spec(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+								  const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+								  uint8_t *__restrict__ ws, const uint32_t *__restrict__ hl, uint32_t nh,
+								  uint8_t *__restrict__ hs, const uint64_t *__restrict__ hs_off, uint32_t dbg)
+{
+	uint32_t h = blockIdx.x / DSB_HEAVY_W, part = blockIdx.x % DSB_HEAVY_W, lane = threadIdx.x;
+	if (h >= nh)
+		return;
+	dsb_read_ws w;
+	dsb_rflags_t f;
+	dsb_rstate_t *sp;
+	dsb_heavy_ws(ix, len, ws_off, scale, ws, hl[h], &w, &f, &sp, dbg);
+	__shared__ uint64_t dela_lds[DSB_DELA_LDS_BYTES / 8];
+	dsb_dela_lds(&w, dela_lds);
+	dsb_heavy_rec *rec = (dsb_heavy_rec *)(hs + hs_off[h]);
+	w.sms = (dsb_spd_t *)(hs + hs_off[h] + dsb_al(sizeof(dsb_heavy_rec) * DSB_HEAVY_MAX_HIT) +
+			      part * dsb_al(sizeof(dsb_spd_t) * (uint64_t)w.cap.sms));
+	int key_len = dsb_build_hash_table<true>(&w, (int)w.L); /* built by k_hash_lds: the key length only */
+	for (uint32_t i = part; i < w.n_hit; i += DSB_HEAVY_W) {
+		dsb_heavy_rec *rc = rec + i;
+		if (lane == 0) {
+			rc->ch = w.hit[i];
+			rc->flags = 0;
+		}
+		if (lane < (DSB_HEAVY_MAX_HIT + 63) / 64)
+			rc->bits[lane] = 0;
+		__syncthreads();
+		if (w.hit[i].sum_score == 0)
+			continue; /* never scored (the reference skips it too) */
+		w.spec_ch = &rc->ch;
+		w.spec_bits = rc->bits;
+		w.overflow = 0;
+		int ok = dsb_score_chain<true>(&w, i, w.L, key_len);
+		__syncthreads();
+		if (lane == 0)
+			rc->flags = ok ? 1u : 2u;
+	}
+}
+
+template <int V>
+__global__ __launch_bounds__(64, 4) void k_heavy_fin(const dsb_dindex_t *__restrict__ ix, const uint32_t *__restrict__ len,
+								 const uint64_t *__restrict__ ws_off, const uint32_t *__restrict__ scale,
+								 uint8_t *__restrict__ ws, const uint32_t *__restrict__ hl, uint32_t nh,
+								 uint8_t *__restrict__ hs, const uint64_t *__restrict__ hs_off,
+								 dsb_read_out_t *__restrict__ ro, uint32_t *__restrict__ n_overflow, uint32_t dbg)
+{
+	uint32_t h = blockIdx.x, lane = threadIdx.x;
+	if (h >= nh)
+		return;
+	uint32_t r = hl[h];
+	dsb_read_ws w;
+	dsb_rflags_t f;
+	dsb_rstate_t *sp;
+	dsb_heavy_ws(ix, len, ws_off, scale, ws, r, &w, &f, &sp, dbg);
+	__shared__ uint64_t dela_lds[DSB_DELA_LDS_BYTES / 8];
+	dsb_dela_lds(&w, dela_lds);
+	const dsb_heavy_rec *rec = (const dsb_heavy_rec *)(hs + hs_off[h]);
+	int key_len = dsb_build_hash_table<true>(&w, (int)w.L);
+	constexpr uint32_t NW = (DSB_HEAVY_MAX_HIT + 63) / 64;
+	for (uint32_t i = 0; i < w.n_hit; i++) {
+		if (w.hit[i].sum_score == 0)
+			continue;
+		const dsb_heavy_rec *rc = rec + i;
+		/* valid: scored without overflow, and every chain it merged still live */
+		uint64_t word = lane < NW ? rc->bits[lane] : 0;
+		int bad = 0;
+		for (uint64_t m = word; m; m &= m - 1)
+			bad |= w.hit[lane * 64 + (uint32_t)__builtin_ctzll(m)].sum_score == 0;
+		int valid = rc->flags == 1 && dsb_wballot(bad) == 0;
+		if (valid) {
+			__syncthreads();
+			if (lane == 0)
+				w.hit[i] = rc->ch;
+			for (uint64_t m = word; m; m &= m - 1) { /* the merged chains, zeroed as dsb_comb_merge does */
+				dsb_chain_t *c = w.hit + lane * 64 + (uint32_t)__builtin_ctzll(m);
+				c->sum_score = 0;
+				c->t_st = c->t_ed = c->q_st = c->q_ed = 0;
+			}
+			__syncthreads();
+		} else if (!dsb_score_chain<true>(&w, i, w.L, key_len))
+			break; /* overflow: the read is re-run (kernels.hip batch_run) */
+	}
+	if (!w.overflow)
+		dsb_dela_post(&w);
+	__syncthreads();
+	if (lane == 0) {
+		dsb_state_save(&w, &f, sp);
+		dsb_read_out_t o;
+		o.n_hit = w.n_hit;
+		o.n_anchor = w.n_anc;
+		o.fast = w.fast_classify;
+		o.status = w.overflow;
+		o.reached_update = w.reached_update;
+		o.pad = 0;
+		o.hit_off = 0;
+		ro[r] = o;
+		if (w.overflow)
+			atomicAdd(n_overflow, 1u);
+	}
+}
+
 #endif

@@ -106,6 +106,8 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 	w->lds_hb = 0;
 	w->lds_cand = 0;
 	w->lds_q = 0;
+	w->spec_ch = 0;
+	w->spec_bits = 0;
 	uint32_t *h = (uint32_t *)(base + o.hash);
 	uint64_t hs = 1ull << o.kl;
 	for (int s = 0; s < 2; s++) {

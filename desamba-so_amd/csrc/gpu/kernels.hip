@@ -266,13 +266,15 @@ struct dsb_gpu_dev {
 	int slot;                /* index in dsb_index.gpus */
 	hipStream_t stream;
 	hipStream_t stream2;     /* scoring of the reads that skip slow seeding, beside the slow phases */
-	hipEvent_t ev_a, ev_b, ev_fork, ev_r0, ev_r1;
+	hipStream_t stream3;     /* the heavy reads' scoring, beside both (run_split) */
+	hipEvent_t ev_a, ev_b, ev_fork, ev_r0, ev_r1, ev_h0, ev_h1;
 	pthread_mutex_t mu;
 	dsb_dindex_t h;          /* host copy holding device pointers */
 	dsb_dindex_t *d;         /* device copy */
 	std::vector<void *> allocs;
 	dbuf ws_off, scale, ws, wsr, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2;
 	dbuf vlen, vso, vidx, vtid; /* the deferred overflow re-runs of a batch (batch_run) */
+	dbuf hscr, hoff;         /* the heavy reads' scoring scratch and its per-read offsets (run_split) */
 	hipEvent_t evh[2][2];    /* k_hash_lds before the scoring launch, per stream (launch_phase) */
 	int evh_used[2] = {0, 0};
 	/* streamed batches (read_classify pipeline): uploads on their own stream through pinned
@@ -361,7 +363,10 @@ static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu
 		int least = 0, greatest = 0;
 		HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
 		HIP_OK(hipStreamCreateWithPriority(&g->stream2, hipStreamNonBlocking, least));
+		HIP_OK(hipStreamCreateWithPriority(&g->stream3, hipStreamNonBlocking, greatest));
 	}
+	HIP_OK(hipEventCreate(&g->ev_h0));
+	HIP_OK(hipEventCreate(&g->ev_h1));
 	HIP_OK(hipEventCreate(&g->ev_fork));
 	HIP_OK(hipEventCreate(&g->ev_r0));
 	HIP_OK(hipEventCreate(&g->ev_r1));
@@ -578,7 +583,7 @@ static void dev_free(dsb_gpu_dev *g)
 	for (void *p : g->allocs)
 		hipFree(p);
 	dbuf *bs[] = {&g->ws_off, &g->scale, &g->ws, &g->wsr, &g->order, &g->word_off, &g->ro, &g->mrl, &g->hits,
-		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2};
+		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2, &g->hscr, &g->hoff};
 	for (dbuf *b : bs)
 		b->release();
 	hipEventDestroy(g->ev_a);
@@ -586,10 +591,13 @@ static void dev_free(dsb_gpu_dev *g)
 	hipEventDestroy(g->ev_fork);
 	hipEventDestroy(g->ev_r0);
 	hipEventDestroy(g->ev_r1);
+	hipEventDestroy(g->ev_h0);
+	hipEventDestroy(g->ev_h1);
 	for (int k = 0; k < 2; k++)
 		for (int e = 0; e < 2; e++)
 			hipEventDestroy(g->evh[k][e]);
 	hipStreamDestroy(g->stream2);
+	hipStreamDestroy(g->stream3);
 	hipStreamDestroy(g->stream);
 	pthread_mutex_destroy(&g->mu);
 	delete g;
@@ -804,6 +812,7 @@ static uint64_t next_launch_tag(void) { return ++g_launch_tag; }
  * scoring phase's (the callers time the hash build + scoring launch pair together); the events
  * of launches the callers do not time (overflow re-runs) are dropped with clear = 1 */
 #define DSB_PH_HASH 9
+#define DSB_PH_HEAVY 10 /* ms_phase: the heavy reads' scoring (run_split), hash build included */
 static float hash_ms(dsb_gpu_dev *g, int clear = 0)
 {
 	float tot = 0;
@@ -942,13 +951,30 @@ static int batch_upload(dsb_gpu_dev *g, const dsb_reads_t *reads, dsb_gpu_batch 
 /* after resolve_f: reads[order[t]] -> slow list (slow seeding still to run) or rest list (scoring
  * next); one atomic per wave, lane order kept inside a wave (per-read results do not depend on
  * the processing order) */
+/* The split's lists: the slow reads, and the scoring reads with the heavy ones (many chains of a
+ * long read: their scoring is a long single-wave tail, ~150 ms on the C2-scale proxy) first, so
+ * that they start with the grid instead of after it. */
+#ifndef DSB_HEAVY_COST
+#define DSB_HEAVY_COST (1u << 20) /* chains x read length: ~130 chains of an 8-kb read */
+#endif
+static uint32_t heavy_cost(void)
+{
+	static int64_t v = -1;
+	if (v < 0) {
+		const char *e = getenv("DSB_HEAVY_COST");
+		v = e ? strtoll(e, NULL, 10) : DSB_HEAVY_COST;
+	}
+	return (uint32_t)v;
+}
+
 __global__ __launch_bounds__(64) void k_split(const uint32_t *__restrict__ len, const uint64_t *__restrict__ ws_off,
 					      const uint32_t *__restrict__ scale, const uint8_t *__restrict__ ws,
 					      const uint32_t *__restrict__ order, uint32_t n, uint32_t *__restrict__ slow_list,
-					      uint32_t *__restrict__ rest_list, uint32_t *__restrict__ cnt2)
+					      uint32_t *__restrict__ heavy_list, uint32_t *__restrict__ rest_list,
+					      uint32_t *__restrict__ cnt3, uint32_t heavy)
 {
 	uint32_t t = blockIdx.x * 64 + threadIdx.x, lane = threadIdx.x;
-	int act = t < n, slow = 0;
+	int act = t < n, slow = 0, hv = 0;
 	uint32_t r = 0;
 	if (act) {
 		r = order[t];
@@ -956,18 +982,23 @@ __global__ __launch_bounds__(64) void k_split(const uint32_t *__restrict__ len, 
 		dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, scale[r]));
 		const dsb_rstate_t *sp = (const dsb_rstate_t *)(ws + ws_off[r] + lay.state);
 		slow = !sp->f.done && !sp->overflow && sp->f.run_slow;
+		hv = !slow && !sp->f.done && !sp->overflow && sp->n_hit && (uint64_t)DSB_MIN(sp->n_hit, 400u) * L >= heavy;
 	}
-	uint64_t ms = __ballot(act && slow), mr = __ballot(act && !slow);
-	uint32_t bs = 0, br = 0;
+	uint64_t ms = __ballot(act && slow), mr = __ballot(act && !slow && !hv), mh = __ballot(act && hv);
+	uint32_t bs = 0, br = 0, bh = 0;
 	if (lane == 0) {
-		bs = atomicAdd(cnt2, (uint32_t)__builtin_popcountll(ms));
-		br = atomicAdd(cnt2 + 1, (uint32_t)__builtin_popcountll(mr));
+		bs = atomicAdd(cnt3, (uint32_t)__builtin_popcountll(ms));
+		br = atomicAdd(cnt3 + 1, (uint32_t)__builtin_popcountll(mr));
+		bh = atomicAdd(cnt3 + 2, (uint32_t)__builtin_popcountll(mh));
 	}
 	bs = (uint32_t)__shfl((int)bs, 0);
 	br = (uint32_t)__shfl((int)br, 0);
+	bh = (uint32_t)__shfl((int)bh, 0);
 	uint64_t lt = lane == 0 ? 0 : (~0ull >> (64 - lane));
 	if (act && slow)
 		slow_list[bs + (uint32_t)__builtin_popcountll(ms & lt)] = r;
+	else if (act && hv)
+		heavy_list[bh + (uint32_t)__builtin_popcountll(mh & lt)] = r;
 	else if (act)
 		rest_list[br + (uint32_t)__builtin_popcountll(mr & lt)] = r;
 }
@@ -1033,33 +1064,99 @@ static hipError_t copy_wait_g(dsb_gpu_dev *g, void *dst, const void *src, size_t
  * reads are split, the scoring of the rest runs on a second stream while the slow phases and
  * then the slow reads' scoring run on the first.  Returns 1 when the rest of part A ran here,
  * 0 when there was nothing to split (the caller continues phase by phase), -1 on error. */
-static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb, uint32_t cn, dsb_gpu_timing &T,
-		     char *err, size_t errn)
+/* the heavy reads' scoring over several waves per read (dsb_kern.h k_heavy_*); DSB_HEAVY_SPEC=0:
+ * one wave per read, the heavy reads first in the scoring launch */
+extern "C" void dsb_heavy_kernels(dsb_heavy_prep_fn *prep, dsb_heavy_spec_fn *spec, dsb_heavy_fin_fn *fin);
+#ifndef DSB_HEAVY_SPEC_DEFAULT
+#define DSB_HEAVY_SPEC_DEFAULT 0
+#endif
+static int heavy_spec(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("DSB_HEAVY_SPEC");
+		v = e ? (atoi(e) != 0) : DSB_HEAVY_SPEC_DEFAULT;
+	}
+	return v;
+}
+
+static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb, uint32_t cn, const uint32_t *hlen,
+		     const uint32_t *hscale, dsb_gpu_timing &T, char *err, size_t errn)
 {
 	hipStream_t s = g->stream;
-	if (g->slist.ensure(4ull * cn + 4, err, errn) || g->rlist.ensure(4ull * cn + 4, err, errn) ||
+	/* slist: the slow reads, then (at cn) the heavy scoring reads; rlist: the scoring list, the
+	 * other scoring reads first gathered at cn */
+	if (g->slist.ensure(8ull * cn + 8, err, errn) || g->rlist.ensure(8ull * cn + 8, err, errn) ||
 	    g->cnt2.ensure(64, err, errn))
 		return -1;
-	HIP_OK(hipMemsetAsync(g->cnt2.p, 0, 8, s));
+	HIP_OK(hipMemsetAsync(g->cnt2.p, 0, 16, s));
+	uint32_t *hl = g->slist.as<uint32_t>() + cn, *rl = g->rlist.as<uint32_t>() + cn;
 	k_split<<<(cn + 63) / 64, 64, 0, s>>>(cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
-					       g->order.as<uint32_t>(), cn, g->slist.as<uint32_t>(), g->rlist.as<uint32_t>(),
-					       g->cnt2.as<uint32_t>());
+					       g->order.as<uint32_t>(), cn, g->slist.as<uint32_t>(), hl, rl,
+					       g->cnt2.as<uint32_t>(), heavy_cost());
 	HIP_OK(hipGetLastError());
-	uint32_t c2[2] = {0, 0};
-	HIP_OK(copy_wait_g(g, c2, g->cnt2.p, 8, hipMemcpyDeviceToHost, s));
-	if (c2[0] + c2[1] != cn) {
-		snprintf(err, errn, "split: %u + %u reads for a chunk of %u", c2[0], c2[1], cn);
+	uint32_t c3[3] = {0, 0, 0};
+	HIP_OK(copy_wait_g(g, c3, g->cnt2.p, 12, hipMemcpyDeviceToHost, s));
+	if (c3[0] + c3[1] + c3[2] != cn) {
+		snprintf(err, errn, "split: %u + %u + %u reads for a chunk of %u", c3[0], c3[1], c3[2], cn);
 		return -1;
 	}
-	if (c2[0] == 0 || c2[1] == 0)
+	if (c3[0] == 0 || c3[1] + c3[2] == 0)
 		return 0;
+	uint32_t nh = c3[2], nr = c3[1];
+	T.n_heavy += nh;
+	static dsb_heavy_prep_fn k_prep;
+	static dsb_heavy_spec_fn k_spec;
+	static dsb_heavy_fin_fn k_fin;
+	if (!k_prep)
+		dsb_heavy_kernels(&k_prep, &k_spec, &k_fin);
+	const int spec = nh && stats == 0 && heavy_spec();
+	if (spec) { /* the heavy reads' scratch, laid out per read */
+		std::vector<uint32_t> hv(nh);
+		HIP_OK(copy_wait_g(g, hv.data(), hl, 4ull * nh, hipMemcpyDeviceToHost, s));
+		std::vector<uint64_t> ho(nh);
+		uint64_t tot = 0;
+		for (uint32_t k = 0; k < nh; k++) {
+			ho[k] = tot;
+			tot += dsb_heavy_bytes(hlen[hv[k]], hscale[hv[k]]);
+		}
+		if (g->hscr.ensure(tot + 256, err, errn) || g->hoff.ensure(8ull * nh + 8, err, errn))
+			return -1;
+		HIP_OK(copy_wait_g(g, g->hoff.p, ho.data(), 8ull * nh, hipMemcpyHostToDevice, s));
+		if (nr)
+			HIP_OK(hipMemcpyAsync(g->rlist.p, rl, 4ull * nr, hipMemcpyDeviceToDevice, s));
+	} else {
+		nr += nh; /* one list: the heavy reads first */
+		if (nh)
+			HIP_OK(hipMemcpyAsync(g->rlist.p, hl, 4ull * nh, hipMemcpyDeviceToDevice, s));
+		if (c3[1])
+			HIP_OK(hipMemcpyAsync(g->rlist.as<uint32_t>() + nh, rl, 4ull * c3[1], hipMemcpyDeviceToDevice, s));
+	}
+	uint32_t c2[2] = {c3[0], nr};
 	/* slow0's few workgroups are queued before the scoring grid so that they are dispatched first */
 	hipEventRecord(g->ev_fork, s);
 	hipEventRecord(g->ev_a, s);
 	launch_phase(g, DSB_PH_SLOW0, stats, cl, wsb, g->slist.as<uint32_t>(), c2[0]);
+	if (spec) {
+		uint32_t dbg = wave_dbg();
+		HIP_OK(hipStreamWaitEvent(g->stream3, g->ev_fork, 0));
+		hipEventRecord(g->ev_h0, g->stream3);
+		hipLaunchKernelGGL(k_hash_lds<0>, dim3(2 * nh), dim3(DSB_HL_WG), 0, g->stream3, g->d, cl, g->ws_off.as<uint64_t>(),
+				   g->scale.as<uint32_t>(), wsb, hl, nh, g->stats.as<unsigned long long>());
+		hipLaunchKernelGGL(k_prep, dim3(nh), dim3(64), 0, g->stream3, g->d, cl, g->ws_off.as<uint64_t>(),
+				   g->scale.as<uint32_t>(), wsb, hl, nh, dbg);
+		hipLaunchKernelGGL(k_spec, dim3(nh * DSB_HEAVY_W), dim3(64), 0, g->stream3, g->d, cl, g->ws_off.as<uint64_t>(),
+				   g->scale.as<uint32_t>(), wsb, hl, nh, g->hscr.as<uint8_t>(), g->hoff.as<uint64_t>(), dbg);
+		hipLaunchKernelGGL(k_fin, dim3(nh), dim3(64), 0, g->stream3, g->d, cl, g->ws_off.as<uint64_t>(),
+				   g->scale.as<uint32_t>(), wsb, hl, nh, g->hscr.as<uint8_t>(), g->hoff.as<uint64_t>(),
+				   g->ro.as<dsb_read_out_t>(), g->cnt.as<uint32_t>(), dbg);
+		hipEventRecord(g->ev_h1, g->stream3);
+		HIP_OK(hipGetLastError());
+	}
 	HIP_OK(hipStreamWaitEvent(g->stream2, g->ev_fork, 0));
 	hipEventRecord(g->ev_r0, g->stream2);
-	launch_phase(g, DSB_PH_DELA, stats, cl, wsb, g->rlist.as<uint32_t>(), c2[1], g->stream2);
+	if (c2[1])
+		launch_phase(g, DSB_PH_DELA, stats, cl, wsb, g->rlist.as<uint32_t>(), c2[1], g->stream2);
 	hipEventRecord(g->ev_r1, g->stream2);
 	HIP_OK(hipGetLastError());
 	T.ms_phase[DSB_PH_SLOW0] += ev_ms(g);
@@ -1070,13 +1167,18 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 		HIP_OK(hipGetLastError());
 	}
 	HIP_OK(hipStreamWaitEvent(s, g->ev_r1, 0));
+	if (spec)
+		HIP_OK(hipStreamWaitEvent(s, g->ev_h1, 0));
 	hipEventRecord(g->ev_b, s);
 	HIP_OK(hipEventSynchronize(g->ev_b));
-	float wall = 0, rest = 0;
+	float wall = 0, rest = 0, heavy = 0;
 	hipEventElapsedTime(&wall, g->ev_fork, g->ev_b);
 	hipEventElapsedTime(&rest, g->ev_r0, g->ev_r1);
+	if (spec)
+		hipEventElapsedTime(&heavy, g->ev_h0, g->ev_h1);
 	T.ms_phase[DSB_PH_DELA] += rest; /* both scoring launches; ms_classA takes the overlapped wall time */
-	{
+	T.ms_phase[DSB_PH_HEAVY] += heavy;
+	if (c2[1]) {
 		float hm = hash_ms(g); /* both launches' read-hash builds (each timed with its scoring launch) */
 		T.ms_phase[DSB_PH_HASH] += hm;
 		T.ms_phase[DSB_PH_DELA] -= hm;
@@ -1389,7 +1491,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			}
 			HIP_OK(hipGetLastError());
 			if (ph == DSB_PH_RESOLVE_F && split_slow()) {
-				int r = run_split(g, stats_on, cl, wsb, cn, T, err, errn);
+				int r = run_split(g, stats_on, cl, wsb, cn, len.data() + cb, scale.data() + cb, T, err, errn);
 				if (r < 0)
 					return -1;
 				if (r == 1) /* the rest of part A ran split */

@@ -41,3 +41,14 @@ extern "C" dsb_phase_fn DSB_CAT(dsb_phase_kernel_, DSB_PH)(int wave, int stats)
 #endif
 #endif
 }
+
+#if DSB_PH == 8
+static_assert(DSB_PH_DELA == 8, "the heavy reads' scoring kernels live in the scoring phase's unit");
+/* the heavy reads' scoring (dsb_kern.h k_heavy_*), for kernels.hip run_split */
+extern "C" void dsb_heavy_kernels(dsb_heavy_prep_fn *prep, dsb_heavy_spec_fn *spec, dsb_heavy_fin_fn *fin)
+{
+	*prep = k_heavy_prep<0>;
+	*spec = k_heavy_spec<0>;
+	*fin = k_heavy_fin<0>;
+}
+#endif

@@ -16,7 +16,7 @@ FMT_SAM, FMT_SAM_FULL, FMT_DES, FMT_DES_FULL = 1, 2, 3, 4
 PHASES = ["island", "fast0", "fast1", "resolve_f", "slow0", "resolve_s0", "slow1", "resolve_s1", "delA"]
 # ms_phase slots: the phases (each with a work-counter block), then the scoring's read-hash build in
 # LDS (k_hash_lds, DSB_HASH_LDS builds; its counters are in the delA block, hash_b)
-MS_PHASES = PHASES + ["hash"]
+MS_PHASES = PHASES + ["hash", "heavy"]
 ST_NAMES = ["occ", "occ_nib", "mem_search", "sa", "uni", "ref_pos", "getref_b", "anchor", "chain", "ek1", "ek2",
             "hash_b", "lookup", "node", "t_mem", "t_map", "t_build", "t_match", "t_win", "t_all", "t_dpm", "t_dps",
             "t_fill", "pass2", "replay", "t_mprobe", "t_mwalk", "t_comb", "nwin", "nbatch", "ncand", "nsms"]
@@ -34,7 +34,7 @@ class Timing(C.Structure):
                 ("ms_parse", C.c_double), ("ms_gather", C.c_double), ("ms_format", C.c_double),
                 ("ms_wait_gpu", C.c_double), ("n_batches", C.c_uint64), ("n_devices", C.c_uint64),
                 ("n_view_records", C.c_uint64), ("n_copied_records", C.c_uint64),
-                ("n_ws_shrink", C.c_uint64)]
+                ("n_ws_shrink", C.c_uint64), ("n_heavy", C.c_uint64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("stats", "ms_phase")}

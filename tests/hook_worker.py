@@ -38,7 +38,7 @@ def main():
                 out, tm, _ = idx.classify(data, fmt=spec.get("fmt", P.FMT_SAM))
             with open(f"{spec['out']}.{k}", "wb") as f:
                 f.write(out)
-            summary["calls"].append({k2: tm[k2] for k2 in ("n_retry", "n_chunks", "n_batches", "n_devices")
+            summary["calls"].append({k2: tm[k2] for k2 in ("n_retry", "n_chunks", "n_batches", "n_devices", "n_heavy")
                                      if k2 in tm})
     finally:
         idx.close()

@@ -113,6 +113,26 @@ def test_deferred_reruns_in_groups(fixture_index, tmp_path):
     assert got[0] == want[0]
 
 
+@pytest.mark.parametrize("cost", ["1", "300000"])
+def test_heavy_reads_scored_over_waves_byte_identical(fixture_index, tmp_path, cost):
+    """The heavy reads' scoring (dsb_kern.h k_heavy_prep / k_heavy_spec / k_heavy_fin): every chain
+    of a read scored speculatively on its own wave, then accepted in chain order or scored again.
+    DSB_HEAVY_COST=1 sends every read with a chain that way (300000: the longer / many-chain
+    ones); records byte-identical to the one-wave-per-read scoring (DSB_HEAVY_SPEC=0), batch and
+    text paths."""
+    fq = tmp_path / "ont_x2.fq"
+    fq.write_bytes(golden("ont.fq") * 2)
+    for mode in ("batch", "text"):
+        want, _ = run_worker(tmp_path, f"one_{mode}", fixture_index, [fq], {"DSB_HEAVY_SPEC": "0"}, lib=PROD_LIB,
+                             mode=mode)
+        got, s = run_worker(tmp_path, f"heavy_{mode}_{cost}", fixture_index, [fq], {"DSB_HEAVY_COST": cost, "DSB_HEAVY_SPEC": "1"},
+                            lib=PROD_LIB, mode=mode)
+        nh = sum(c.get("n_heavy", 0) for c in s["calls"])
+        print(f"{mode} cost {cost}: {nh} heavy reads")
+        assert nh > 0, s["calls"]
+        assert got[0] == want[0], (mode, cost)
+
+
 def test_sp_set_pool_sets_never_match_stale_slots(fixture_index, tmp_path):
     """Regression test for round 3's lost-anchor race, in its round-4 form: the seeding sp_set
     slots are never cleared; they live in a per-GPU pool of wave-sized sets that seeding waves take
