@@ -2066,10 +2066,14 @@ DSB_HD void dsb_chain_insert_M2(dsb_read_ws *w, uint32_t ai)
  * (ref_ID, direction, ref_offset).  WAVE: bitonic sort of (key, index) pairs (a total order,
  * so the same permutation as any stable sort), keys/indices staged in hit_tmp. */
 #define DSB_SORT_LDS 512
-/* the slow-mode resolves (RESOLVE_S0/S1: ~2% of the reads, a few with thousands of anchors whose
- * sorts and chain_insert_M3 DP ran from HBM on one wave, ~64 ms per chunk for one read): sorts
- * of up to 4096 anchors and DP segments of up to the reference's 1024 anchors in LDS (48 KB) */
-#define DSB_SORT_LDS_SLOW 4096
+/* the slow-mode resolves' LDS sorts (RESOLVE_S0/S1: ~2% of the reads, a few with thousands of
+ * anchors).  4096 entries (48 KB: sorts of up to 4096 anchors and M3 segments of up to the
+ * reference's 1024 anchors in LDS) took one read's 64-85 ms per chunk out of HBM, but a 48-KB
+ * workgroup waits for a CU with that much LDS free beside the scoring grid of the split: on the C2
+ * proxy resolve_s0 + resolve_s1 231 + 50 ms per step at 4096 vs 175 + 2 at 512 (r05_u, 5 steps) */
+#ifndef DSB_SORT_LDS_SLOW
+#define DSB_SORT_LDS_SLOW 512
+#endif
 template <bool WAVE>
 DSB_HD void dsb_sort_anchors(dsb_read_ws *w)
 {

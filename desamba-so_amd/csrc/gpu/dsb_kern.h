@@ -27,10 +27,10 @@
 #ifndef DSB_MINW_RESOLVE
 #define DSB_MINW_RESOLVE 4
 #endif
-/* the slow resolves hold 48 KB of LDS per wave (DSB_SORT_LDS_SLOW): at most 3 per CU anyway */
+/* slow resolves built with 48 KB of LDS per wave (DSB_SORT_LDS_SLOW 4096): at most 3 per CU anyway */
 #define DSB_MINW_WAVE(PH) ((PH) == DSB_PH_DELA ? DSB_MINW_DELA : \
 			   ((PH) == DSB_PH_FAST0 || (PH) == DSB_PH_FAST1 || (PH) == DSB_PH_SLOW0 || (PH) == DSB_PH_SLOW1) \
-			   ? DSB_MINW_FAST : ((PH) == DSB_PH_RESOLVE_S0 || (PH) == DSB_PH_RESOLVE_S1) ? 1 : DSB_MINW_RESOLVE)
+			   ? DSB_MINW_FAST : (((PH) == DSB_PH_RESOLVE_S0 || (PH) == DSB_PH_RESOLVE_S1) && DSB_SORT_LDS_SLOW > 1024) ? 1 : DSB_MINW_RESOLVE)
 #define DSB_WIN_LDS_BYTES ((DSB_WIN_BYTES + 15) & ~15)
 /* The scoring phase's reference windows (sdp_middle ref[2000], sdp_right/left ref[1000]) live in
  * LDS, in the same 4 KB the read-hash build uses for its key-group slots before the first window

@@ -266,7 +266,8 @@ struct dsb_gpu_dev {
 	int slot;                /* index in dsb_index.gpus */
 	hipStream_t stream;
 	hipStream_t stream2;     /* scoring of the reads that skip slow seeding, beside the slow phases */
-	hipStream_t stream3;     /* the heavy reads' scoring, beside both (run_split) */
+	hipStream_t stream3 = nullptr; /* the heavy reads' scoring, beside both (run_split, DSB_HEAVY_SPEC) */
+	int prio_hi = 0;
 	hipEvent_t ev_a, ev_b, ev_fork, ev_r0, ev_r1, ev_h0, ev_h1;
 	pthread_mutex_t mu;
 	dsb_dindex_t h;          /* host copy holding device pointers */
@@ -363,7 +364,7 @@ static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu
 		int least = 0, greatest = 0;
 		HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
 		HIP_OK(hipStreamCreateWithPriority(&g->stream2, hipStreamNonBlocking, least));
-		HIP_OK(hipStreamCreateWithPriority(&g->stream3, hipStreamNonBlocking, greatest));
+		g->prio_hi = greatest; /* stream3 is created on first use (run_split, DSB_HEAVY_SPEC) */
 	}
 	HIP_OK(hipEventCreate(&g->ev_h0));
 	HIP_OK(hipEventCreate(&g->ev_h1));
@@ -597,7 +598,8 @@ static void dev_free(dsb_gpu_dev *g)
 		for (int e = 0; e < 2; e++)
 			hipEventDestroy(g->evh[k][e]);
 	hipStreamDestroy(g->stream2);
-	hipStreamDestroy(g->stream3);
+	if (g->stream3)
+		hipStreamDestroy(g->stream3);
 	hipStreamDestroy(g->stream);
 	pthread_mutex_destroy(&g->mu);
 	delete g;
@@ -1111,6 +1113,8 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 	if (!k_prep)
 		dsb_heavy_kernels(&k_prep, &k_spec, &k_fin);
 	const int spec = nh && stats == 0 && heavy_spec();
+	if (spec && !g->stream3)
+		HIP_OK(hipStreamCreateWithPriority(&g->stream3, hipStreamNonBlocking, g->prio_hi));
 	if (spec) { /* the heavy reads' scratch, laid out per read */
 		std::vector<uint32_t> hv(nh);
 		HIP_OK(copy_wait_g(g, hv.data(), hl, 4ull * nh, hipMemcpyDeviceToHost, s));
