@@ -66,10 +66,10 @@ for step in "$@"; do
 		timeout -k 10 900 $PY -m pytest tests/test_gpu_scale.py -x -v -s ${rest:+-k "$rest"} --timeout 600 --timeout-method thread > "$O/scale.log" 2>&1 || { tail -40 "$O/scale.log"; exit 1; }
 		grep -E "PASSED|FAILED|SKIPPED|T3 mismatches" "$O/scale.log" | tail -20 ;;
 	tests) # tests:FILE,FILE  (paths under tests/)
-		timeout -k 10 600 $PY -u -m pytest ${rest//,/ } -x -v --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 || { tail -40 "$O/tests.log"; exit 1; }
+		timeout -k 10 1000 $PY -u -m pytest ${rest//,/ } -x -v -s --timeout 600 --timeout-method thread > "$O/tests.log" 2>&1 || { tail -40 "$O/tests.log"; exit 1; }
 		grep -E "PASSED|FAILED|SKIPPED|ERROR" "$O/tests.log" | tail -30 ;;
 	suite)
-		timeout -k 10 1000 $PY -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > "$O/suite.log" 2>&1 || { tail -40 "$O/suite.log"; exit 1; }
+		timeout -k 10 1100 $PY -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread > "$O/suite.log" 2>&1 || { tail -40 "$O/suite.log"; exit 1; }
 		tail -3 "$O/suite.log" ;;
 	prof)
 		rest=${rest//=/ }
