@@ -276,6 +276,7 @@ struct dsb_gpu_dev {
 	dbuf ws_off, scale, ws, wsr, order, word_off, ro, mrl, hits, hit_off, cnt, stats, sel, wo2, slist, rlist, cnt2;
 	dbuf vlen, vso, vidx, vtid; /* the deferred overflow re-runs of a batch (batch_run) */
 	dbuf hscr, hoff;         /* the heavy reads' scoring scratch and its per-read offsets (run_split) */
+	dbuf blist;              /* the scoring reads by cost class, DSB_COST_CLASSES lists of a chunk each (run_split) */
 	hipEvent_t evh[2][2];    /* k_hash_lds before the scoring launch, per stream (launch_phase) */
 	int evh_used[2] = {0, 0};
 	/* streamed batches (read_classify pipeline): uploads on their own stream through pinned
@@ -584,7 +585,7 @@ static void dev_free(dsb_gpu_dev *g)
 	for (void *p : g->allocs)
 		hipFree(p);
 	dbuf *bs[] = {&g->ws_off, &g->scale, &g->ws, &g->wsr, &g->order, &g->word_off, &g->ro, &g->mrl, &g->hits,
-		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2, &g->hscr, &g->hoff};
+		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2, &g->hscr, &g->hoff, &g->blist};
 	for (dbuf *b : bs)
 		b->release();
 	hipEventDestroy(g->ev_a);
@@ -953,12 +954,16 @@ static int batch_upload(dsb_gpu_dev *g, const dsb_reads_t *reads, dsb_gpu_batch 
 /* after resolve_f: reads[order[t]] -> slow list (slow seeding still to run) or rest list (scoring
  * next); one atomic per wave, lane order kept inside a wave (per-read results do not depend on
  * the processing order) */
-/* The split's lists: the slow reads, and the scoring reads with the heavy ones (many chains of a
- * long read: their scoring is a long single-wave tail, ~150 ms on the C2-scale proxy) first, so
- * that they start with the grid instead of after it. */
+/* The split's lists: the slow reads, and the scoring reads in descending classes of their
+ * estimated scoring cost (chains x read length, powers of two): the longest waves start first, so
+ * the launch does not end on a few of them (longest-processing-time-first).  On the C2 proxy
+ * (5-step A/B, r05_hc) with one class of reads >= 2^16 first the scoring fell 431 -> 386 ms per
+ * step; reads with no scoring to do cost 0.  With DSB_HEAVY_SPEC the reads of cost >=
+ * DSB_HEAVY_COST go to their own list (scored over several waves each). */
 #ifndef DSB_HEAVY_COST
 #define DSB_HEAVY_COST (1u << 20) /* chains x read length: ~130 chains of an 8-kb read */
 #endif
+#define DSB_COST_CLASSES 14 /* class 0: cost < 2^12; class c: [2^(c+11), 2^(c+12)); the last open-ended */
 static uint32_t heavy_cost(void)
 {
 	static int64_t v = -1;
@@ -968,41 +973,59 @@ static uint32_t heavy_cost(void)
 	}
 	return (uint32_t)v;
 }
+DSB_HD uint32_t dsb_cost_class(uint64_t cost)
+{
+	if (cost < (1u << 12))
+		return 0;
+	uint32_t c = 63 - (uint32_t)__builtin_clzll(cost) - 11;
+	return c < DSB_COST_CLASSES - 1 ? c : DSB_COST_CLASSES - 1;
+}
 
+/* cnt: [0] slow, [1] heavy (spec), [2 + c] class c; class c's reads at classes + c * n */
 __global__ __launch_bounds__(64) void k_split(const uint32_t *__restrict__ len, const uint64_t *__restrict__ ws_off,
 					      const uint32_t *__restrict__ scale, const uint8_t *__restrict__ ws,
 					      const uint32_t *__restrict__ order, uint32_t n, uint32_t *__restrict__ slow_list,
-					      uint32_t *__restrict__ heavy_list, uint32_t *__restrict__ rest_list,
-					      uint32_t *__restrict__ cnt3, uint32_t heavy)
+					      uint32_t *__restrict__ heavy_list, uint32_t *__restrict__ classes,
+					      uint32_t *__restrict__ cnt, uint32_t heavy)
 {
 	uint32_t t = blockIdx.x * 64 + threadIdx.x, lane = threadIdx.x;
 	int act = t < n, slow = 0, hv = 0;
-	uint32_t r = 0;
+	uint32_t r = 0, cls = 0;
 	if (act) {
 		r = order[t];
 		uint32_t L = len[r];
 		dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, scale[r]));
 		const dsb_rstate_t *sp = (const dsb_rstate_t *)(ws + ws_off[r] + lay.state);
 		slow = !sp->f.done && !sp->overflow && sp->f.run_slow;
-		hv = !slow && !sp->f.done && !sp->overflow && sp->n_hit && (uint64_t)DSB_MIN(sp->n_hit, 400u) * L >= heavy;
+		uint64_t cost = (!slow && !sp->f.done && !sp->overflow) ? (uint64_t)DSB_MIN(sp->n_hit, 400u) * L : 0;
+		hv = !slow && sp->n_hit && cost >= heavy;
+		cls = dsb_cost_class(cost);
 	}
-	uint64_t ms = __ballot(act && slow), mr = __ballot(act && !slow && !hv), mh = __ballot(act && hv);
-	uint32_t bs = 0, br = 0, bh = 0;
-	if (lane == 0) {
-		bs = atomicAdd(cnt3, (uint32_t)__builtin_popcountll(ms));
-		br = atomicAdd(cnt3 + 1, (uint32_t)__builtin_popcountll(mr));
-		bh = atomicAdd(cnt3 + 2, (uint32_t)__builtin_popcountll(mh));
-	}
-	bs = (uint32_t)__shfl((int)bs, 0);
-	br = (uint32_t)__shfl((int)br, 0);
-	bh = (uint32_t)__shfl((int)bh, 0);
 	uint64_t lt = lane == 0 ? 0 : (~0ull >> (64 - lane));
-	if (act && slow)
-		slow_list[bs + (uint32_t)__builtin_popcountll(ms & lt)] = r;
-	else if (act && hv)
-		heavy_list[bh + (uint32_t)__builtin_popcountll(mh & lt)] = r;
-	else if (act)
-		rest_list[br + (uint32_t)__builtin_popcountll(mr & lt)] = r;
+	/* slow and heavy lists, then each class present in the wave: one atomic per list per wave */
+	int key = !act ? -1 : slow ? DSB_COST_CLASSES : hv ? DSB_COST_CLASSES + 1 : (int)cls;
+	for (;;) {
+		uint64_t live = __ballot(key >= 0);
+		if (!live)
+			break;
+		int k0 = __shfl(key, (int)__builtin_ctzll(live));
+		uint64_t m = __ballot(key == k0);
+		uint32_t *ctr = k0 == DSB_COST_CLASSES ? cnt : k0 == DSB_COST_CLASSES + 1 ? cnt + 1 : cnt + 2 + k0;
+		uint32_t base = 0;
+		if (lane == (uint32_t)__builtin_ctzll(m))
+			base = atomicAdd(ctr, (uint32_t)__builtin_popcountll(m));
+		base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(m));
+		if (key == k0) {
+			uint32_t at = base + (uint32_t)__builtin_popcountll(m & lt);
+			if (k0 == DSB_COST_CLASSES)
+				slow_list[at] = r;
+			else if (k0 == DSB_COST_CLASSES + 1)
+				heavy_list[at] = r;
+			else
+				classes[(uint64_t)k0 * n + at] = r;
+			key = -1;
+		}
+	}
 }
 
 /* The split of part A (run_split): after resolve_f the reads that still need slow seeding run
@@ -1086,33 +1109,50 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 		     const uint32_t *hscale, dsb_gpu_timing &T, char *err, size_t errn)
 {
 	hipStream_t s = g->stream;
-	/* slist: the slow reads, then (at cn) the heavy scoring reads; rlist: the scoring list, the
-	 * other scoring reads first gathered at cn */
-	if (g->slist.ensure(8ull * cn + 8, err, errn) || g->rlist.ensure(8ull * cn + 8, err, errn) ||
-	    g->cnt2.ensure(64, err, errn))
+	/* slist: the slow reads, then (at cn) the heavy scoring reads (DSB_HEAVY_SPEC); blist: the
+	 * other scoring reads by cost class; rlist: those, costliest class first */
+	const int want_spec = stats == 0 && heavy_spec();
+	if (g->slist.ensure(8ull * cn + 8, err, errn) || g->rlist.ensure(4ull * cn + 4, err, errn) ||
+	    g->blist.ensure(4ull * DSB_COST_CLASSES * cn + 4, err, errn) || g->cnt2.ensure(4 * (2 + DSB_COST_CLASSES), err, errn))
 		return -1;
-	HIP_OK(hipMemsetAsync(g->cnt2.p, 0, 16, s));
-	uint32_t *hl = g->slist.as<uint32_t>() + cn, *rl = g->rlist.as<uint32_t>() + cn;
+	HIP_OK(hipMemsetAsync(g->cnt2.p, 0, 4 * (2 + DSB_COST_CLASSES), s));
+	uint32_t *hl = g->slist.as<uint32_t>() + cn;
 	k_split<<<(cn + 63) / 64, 64, 0, s>>>(cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
-					       g->order.as<uint32_t>(), cn, g->slist.as<uint32_t>(), hl, rl,
-					       g->cnt2.as<uint32_t>(), heavy_cost());
+					       g->order.as<uint32_t>(), cn, g->slist.as<uint32_t>(), hl, g->blist.as<uint32_t>(),
+					       g->cnt2.as<uint32_t>(), want_spec ? heavy_cost() : UINT32_MAX);
 	HIP_OK(hipGetLastError());
-	uint32_t c3[3] = {0, 0, 0};
-	HIP_OK(copy_wait_g(g, c3, g->cnt2.p, 12, hipMemcpyDeviceToHost, s));
-	if (c3[0] + c3[1] + c3[2] != cn) {
-		snprintf(err, errn, "split: %u + %u + %u reads for a chunk of %u", c3[0], c3[1], c3[2], cn);
+	uint32_t cc[2 + DSB_COST_CLASSES];
+	HIP_OK(copy_wait_g(g, cc, g->cnt2.p, sizeof(cc), hipMemcpyDeviceToHost, s));
+	uint32_t nr = 0;
+	for (int k = 0; k < DSB_COST_CLASSES; k++)
+		nr += cc[2 + k];
+	uint32_t nh = cc[1];
+	if (cc[0] + nh + nr != cn) {
+		snprintf(err, errn, "split: %u + %u + %u reads for a chunk of %u", cc[0], nh, nr, cn);
 		return -1;
 	}
-	if (c3[0] == 0 || c3[1] + c3[2] == 0)
+	if (cc[0] == 0 || nh + nr == 0)
 		return 0;
-	uint32_t nh = c3[2], nr = c3[1];
-	T.n_heavy += nh;
+	/* the rest of the reads' list, costliest class first */
+	for (int k = DSB_COST_CLASSES - 1, at = 0; k >= 0; k--)
+		if (cc[2 + k]) {
+			HIP_OK(hipMemcpyAsync(g->rlist.as<uint32_t>() + at, g->blist.as<uint32_t>() + (uint64_t)k * cn, 4ull * cc[2 + k],
+					      hipMemcpyDeviceToDevice, s));
+			at += cc[2 + k];
+		}
+	{ /* reads at or above DSB_HEAVY_COST (their own kernels with DSB_HEAVY_SPEC; else first in the list) */
+		uint32_t hc = dsb_cost_class(heavy_cost());
+		uint64_t nheavy = nh;
+		for (int k = (int)hc; k < DSB_COST_CLASSES; k++)
+			nheavy += cc[2 + k];
+		T.n_heavy += nheavy;
+	}
 	static dsb_heavy_prep_fn k_prep;
 	static dsb_heavy_spec_fn k_spec;
 	static dsb_heavy_fin_fn k_fin;
 	if (!k_prep)
 		dsb_heavy_kernels(&k_prep, &k_spec, &k_fin);
-	const int spec = nh && stats == 0 && heavy_spec();
+	const int spec = nh > 0;
 	if (spec && !g->stream3)
 		HIP_OK(hipStreamCreateWithPriority(&g->stream3, hipStreamNonBlocking, g->prio_hi));
 	if (spec) { /* the heavy reads' scratch, laid out per read */
@@ -1127,16 +1167,8 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 		if (g->hscr.ensure(tot + 256, err, errn) || g->hoff.ensure(8ull * nh + 8, err, errn))
 			return -1;
 		HIP_OK(copy_wait_g(g, g->hoff.p, ho.data(), 8ull * nh, hipMemcpyHostToDevice, s));
-		if (nr)
-			HIP_OK(hipMemcpyAsync(g->rlist.p, rl, 4ull * nr, hipMemcpyDeviceToDevice, s));
-	} else {
-		nr += nh; /* one list: the heavy reads first */
-		if (nh)
-			HIP_OK(hipMemcpyAsync(g->rlist.p, hl, 4ull * nh, hipMemcpyDeviceToDevice, s));
-		if (c3[1])
-			HIP_OK(hipMemcpyAsync(g->rlist.as<uint32_t>() + nh, rl, 4ull * c3[1], hipMemcpyDeviceToDevice, s));
 	}
-	uint32_t c2[2] = {c3[0], nr};
+	uint32_t c2[2] = {cc[0], nr};
 	/* slow0's few workgroups are queued before the scoring grid so that they are dispatched first */
 	hipEventRecord(g->ev_fork, s);
 	hipEventRecord(g->ev_a, s);
