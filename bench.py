@@ -590,11 +590,14 @@ def main():
             per_phase["island"]["probes_per_s"] = round(probes / (ms_i / 1e3))
             per_phase["island"]["sector_frac_of_random_line_peak"] = round(
                 64 * probes / (ms_i / 1e3) / 1e9 / RANDOM_LINE_PEAK_GBS, 4)
-        # no phase can beat the chip: an achieved rate above its peak is an accounting error
+        # no phase can beat the chip: an achieved rate above its peak is an accounting error — recorded
+        # in the line (roofline.accounting_error) and on stderr, without losing the run's measurements
+        accounting_error = []
         for ph, v in per_phase.items():
             for key in ("achieved_GBs", "sector_GBs"):
-                if v.get(key) is not None:
-                    assert v[key] <= HBM_PEAK_GBS, f"roofline accounting: {ph} {key} {v[key]} > {HBM_PEAK_GBS} GB/s"
+                if v.get(key) is not None and v[key] > HBM_PEAK_GBS:
+                    accounting_error.append(f"{ph} {key} {v[key]} > {HBM_PEAK_GBS} GB/s")
+                    print(f"[bench] roofline accounting error: {accounting_error[-1]}", file=sys.stderr)
         tj = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
         if os.path.exists(tf):
@@ -648,6 +651,8 @@ def main():
                         "frac": round(step_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4)}
         roof["phases"] = per_phase
         roof["traffic_profile"] = (tj or {}).get("tag")
+        if accounting_error:
+            roof["accounting_error"] = accounting_error
         stats = {"phases": ts["stats_phase"], "classB": ts["stats_B"]}
 
     cpu = dropin = t3 = None

@@ -97,6 +97,8 @@ typedef struct {
 	const uint32_t *pre;    /* k-mer & 0x3FFFFFF per position (K_seed output): F at [0, L), R at [L, 2L) */
 	dsb_seed_t *seeds;      /* (L>>1)+20 (+spill) entries; R seeds at L>>2 (src/cly.c:1238,1252) */
 	dsb_anchor_t *anc; uint32_t n_anc;
+	uint32_t anc_hw;        /* the most anchors the reference's anchor_v held so far in this read (its capacity
+	                         * is 10 * 2^k above it: the realloc points of kv_pushp_2, dsb_map_seed) */
 	dsb_anchor_t *anc_tmp;
 	dsb_anchor_t *anc_tmp2; /* the seeding state machine's second staging pool (cap.anc entries) */
 	uint32_t *sidx, *stmp;  /* msort permutation scratch (max(anc, hit) entries) */
@@ -785,11 +787,54 @@ DSB_HD void dsb_get_ref_r(dsb_read_ws *w, dsb_w32 &T, uint64_t uni_offset, uint3
 	dsb_w32_put(T, length, lo, hi);
 }
 
+/*
+ * The byte before get_new_ed's q_buff (H1).  lv_extd reads query[-1] on windows of 1-4 bases, and
+ * only that byte of the stale ones can change its result (every other read below the strings is
+ * masked by the '#'/'$' terminators).  In the hermetic build (clang -O2, pattern init) get_new_ed
+ * is an out-of-line function called from map_seed's REF_POS loop; its frame holds t_buff at
+ * rsp+0x08 and q_buff at rsp+0x18, both pattern-initialised, and the 3 padding bytes between them
+ * are not, so q_buff[-1] keeps what the last callee of map_seed at that depth left there:
+ *   - lv_extd (map_seed's prefix / suffix extensions, src/cly.c:767,820) pattern-initialises its
+ *     match_num_data[99], which covers that byte: 0xAA when the REF_POS loop starts;
+ *   - kv_pushp_2's realloc (src/cly.c:921) of the anchor vector when a push finds n == m: glibc
+ *     2.35's realloc stores the old chunk size (8 bytes, < 2^40) across it: 0x00;
+ *   - get_new_ed itself never writes it.
+ * So q_buff[-1] is 0xAA until the first kept REF_POS item of the call whose push grew the vector,
+ * 0x00 after it (dsb_map_seed).  Derived from the objects oracle/Makefile builds
+ * (llvm-objdump / llvm-dwarfdump of _ref/obj_herm/cly.o) and pinned by tools/emu_vs_herm.py.
+ * A realloc(NULL) served from the tcache leaves the byte alone (the first push of a read);
+ * DSB_QB_FIRST_PUSH is what the first push leaves.
+ */
+#define DSB_QB_M1_LOOP 0xAA /* q_buff[-1] before any push of the call grew the anchor vector */
+#define DSB_QB_M1_GROWN 0x00 /* after one did */
+#ifndef DSB_QB_FIRST_PUSH
+#define DSB_QB_FIRST_PUSH DSB_QB_M1_GROWN
+#endif
+/* map_seed's prefix window q_pre sits at rsp+0x78 of its frame in the hermetic build, right above
+ * the spilled s_i pointer (a stack address, top byte 0): q_pre[-1] reads 0x00 */
+#define DSB_QPRE_M1 0x00
+
+/* lv_extd of get_new_ed's left window with q_buff[-1] = qm1; *amb set when the other value of
+ * that byte would give another edit distance (windows of 1-4 bases only) */
+DSB_HD uint32_t dsb_left_lv(const dsb_w32 &T, uint32_t len, dsb_w32 Q, uint32_t qm1, int *amb)
+{
+	dsb_w32_set_byte(Q, -1, qm1);
+	uint32_t ed = (uint32_t)dsb_lv_extd_r(T, (int32_t)len, Q, (int32_t)len);
+	if (amb && len >= 1 && len <= 4) {
+		dsb_w32_set_byte(Q, -1, qm1 == DSB_QB_M1_LOOP ? DSB_QB_M1_GROWN : DSB_QB_M1_LOOP);
+		if ((uint32_t)dsb_lv_extd_r(T, (int32_t)len, Q, (int32_t)len) != ed)
+			*amb = 1;
+	}
+	return ed;
+}
+
 /* get_new_ed, src/cly.c:624-689.  q_buff / t_buff (32-byte stack buffers, pattern-initialised)
  * are register windows; the query of the reverse direction is read in place (two word loads
- * per step), as the reference compares against the read buffer itself. */
+ * per step), as the reference compares against the read buffer itself.  qm1: q_buff[-1] of the
+ * forward (left) call, amb: see dsb_left_lv. */
 DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t *len_, uint32_t *l_mem_ext,
-			    int32_t q_off, uint64_t t_off, uint32_t l_read, int is_FWD)
+			    int32_t q_off, uint64_t t_off, uint32_t l_read, int is_FWD, uint32_t qm1 = DSB_QB_M1_LOOP,
+			    int *amb = 0)
 {
 	dsb_w32 Q = dsb_w32_splat(DSB_STACK_PATTERN), T = Q;
 	const uint8_t *q = q_b;
@@ -837,9 +882,10 @@ DSB_HD void dsb_get_new_ed(dsb_read_ws *w, uint8_t *q_b, uint32_t *e_d, uint32_t
 			}
 		} while (mtc > 0);
 	}
-	if (!is_FWD) /* lv_extd terminates a copy of the read's bytes (q - 8 .. q + 24) */
-		Q = dsb_w32_load(q - 8);
-	*e_d = (uint32_t)dsb_lv_extd_r(T, (int32_t)len, Q, (int32_t)len);
+	if (is_FWD)
+		*e_d = dsb_left_lv(T, len, Q, qm1, amb);
+	else /* lv_extd terminates a copy of the read's bytes (q - 8 .. q + 24) */
+		*e_d = (uint32_t)dsb_lv_extd_r(T, (int32_t)len, dsb_w32_load(q - 8), (int32_t)len);
 	*len_ = len;
 }
 
@@ -915,11 +961,12 @@ DSB_HD void dsb_ned_step(dsb_read_ws *w, dsb_ned_t *e, const uint8_t *q_b)
 	dsb_ned_load(w, e, q_b);
 }
 
-DSB_HD uint32_t dsb_ned_finish(const dsb_ned_t *e)
+DSB_HD uint32_t dsb_ned_finish(const dsb_ned_t *e, uint32_t qm1 = DSB_QB_M1_LOOP, int *amb = 0)
 {
+	if (e->fwd)
+		return dsb_left_lv(e->T, e->len, e->Q, qm1, amb);
 	/* !fwd: lv_extd terminates a copy of the read's bytes (q - 8 .. q + 24) */
-	dsb_w32 Q = e->fwd ? e->Q : dsb_w32_load(e->q - 8);
-	return (uint32_t)dsb_lv_extd_r(e->T, (int32_t)e->len, Q, (int32_t)e->len);
+	return (uint32_t)dsb_lv_extd_r(e->T, (int32_t)e->len, dsb_w32_load(e->q - 8), (int32_t)e->len);
 }
 
 typedef struct { uint8_t *bin_read; uint32_t read_L; uint16_t seed_ID; uint32_t direction; } dsb_seedinfo_t;
@@ -977,6 +1024,7 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 	int32_t s = 0, max_s = 0;
 	/* stack windows q_pre / t_pre / t_suf[LV_L + 1] (src/cly.c:705-707), in registers */
 	dsb_w32 QP = dsb_w32_splat(DSB_STACK_PATTERN), TP = QP, TS = QP;
+	dsb_w32_set_byte(QP, -1, DSB_QPRE_M1);
 	uint64_t lo, hi;
 	do {
 		const uint8_t *q_suf;
@@ -1098,8 +1146,10 @@ DSB_HD void dsb_map_seed_pre(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 	}
 }
 
-/* REF_POS entry rp_s + item of a hit: 1 and the Anchor in *a when the reference pushes one */
-DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, const dsb_seedinfo_t *s_i, dsb_anchor_t *a)
+/* REF_POS entry rp_s + item of a hit: 1 and the Anchor in *a when the reference pushes one.
+ * qm1: get_new_ed's q_buff[-1] for this item; amb: see dsb_left_lv. */
+DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, const dsb_seedinfo_t *s_i, dsb_anchor_t *a,
+			uint32_t qm1 = DSB_QB_M1_LOOP, int *amb = 0)
 {
 	const dsb_dindex_t *ix = w->ix;
 	const int *Q_LV = ix->Q_LV;
@@ -1129,7 +1179,7 @@ DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, c
 				if (R.go) dsb_ned_step(w, &R, s_i->bin_read);
 			}
 			if (cx->ref_l) {
-				am_le = (uint8_t)dsb_ned_finish(&L);
+				am_le = (uint8_t)dsb_ned_finish(&L, qm1, amb);
 				am_ll = (uint8_t)L.len;
 				l_m_ext_l = L.ext;
 			}
@@ -1143,7 +1193,7 @@ DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, c
 			uint32_t ed_l, ed_r, len_l, len_r, l_m_ext_r;
 			if (cx->ref_l) {
 				dsb_get_new_ed(w, s_i->bin_read, &ed_l, &len_l, &l_m_ext_l, cx->q_off, DSB_RP_OFF(rp) + cx->u_off - 1,
-					       s_i->read_L, 1);
+					       s_i->read_L, 1, qm1, amb);
 				am_ll = (uint8_t)len_l;
 				am_le = (uint8_t)ed_l;
 			}
@@ -1177,6 +1227,17 @@ DSB_HD int dsb_map_item(dsb_read_ws *w, const dsb_mapctx_t *cx, uint32_t item, c
 	return 1;
 }
 
+/* kv_pushp_2 (src/lib/kvec.h:103-109) grows the vector when n reaches m: m = 0, 10, 20, 40, ... */
+DSB_HD int dsb_anc_grows(uint32_t n)
+{
+	if (n == 0)
+		return 1;
+	if (n % 10)
+		return 0;
+	n /= 10;
+	return (n & (n - 1)) == 0;
+}
+
 DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i)
 {
 	dsb_mapctx_t cx;
@@ -1184,12 +1245,19 @@ DSB_HDN int32_t dsb_map_seed(dsb_read_ws *w, dsb_mem_t *m_r, dsb_seedinfo_t *s_i
 	if (cx.n_items == 0)
 		return cx.ret;
 	int32_t max_s = 0;
+	/* the reference's anchor_v: n = w->n_anc, capacity m = 0, 10, 20, 40 ... the least one >= every n
+	 * it held; kv_pushp_2 reallocs when a push finds n == m, and from then on get_new_ed's
+	 * q_buff[-1] reads what realloc left (dsb_left_lv) */
+	uint32_t hw = DSB_MAX(w->anc_hw, w->n_anc), qm1 = DSB_QB_M1_LOOP;
 	for (uint32_t it = 0; it < cx.n_items; it++) {
 		dsb_anchor_t an;
-		if (!dsb_map_item(w, &cx, it, s_i, &an))
+		if (!dsb_map_item(w, &cx, it, s_i, &an, qm1))
 			continue;
 		max_s = DSB_MAX(max_s, (int32_t)an.score);
+		if (w->n_anc == hw && dsb_anc_grows(hw))
+			qm1 = hw == 0 ? DSB_QB_FIRST_PUSH : DSB_QB_M1_GROWN;
 		dsb_anchor_t *a = dsb_push_anchor(w);
+		hw = DSB_MAX(hw, w->n_anc);
 		if (!a)
 			return max_s;
 		if (w->stats) w->stats[DSB_ST_ANCHOR]++;
@@ -1495,6 +1563,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 	int st = DSB_SM_DONE;
 	uint32_t ci = 0, a_b = 0, seed_off = 0;
 	int j = 0, skip = 0, n_m = 0, k_map = 0, max_score = 0, string_index = 0, match_len = 0, row_single = 0;
+	int seed_amb = 0; /* an item of the seed read q_buff[-1] where it matters: replayed in order (dsb_map_seed) */
 	uint64_t sp = 0, ep = 0, row = 0, row_end = 0, ss_sp = 0, sa_sp = 0;
 	int ss_len = 0, ss_max = 0, sa_sp_l = 0, l_max = 0;
 	const uint8_t *str = bin_read, *ss_str = bin_read;
@@ -1510,6 +1579,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 		seed_off = c_sv_->offset;                                      \
 		j = (int)c_sv_->len - 1;                                       \
 		skip = 0;                                                      \
+		seed_amb = 0;                                                  \
 		n_top = 0;                                                     \
 		total = 0;                                                     \
 		a_b = w->n_anc;                                                \
@@ -1626,9 +1696,14 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 				dsb_seedinfo_t os = {bin_read, w->L, (uint16_t)(pk3 >> 16), s_d->direction};
 				dsb_anchor_t an;
 				uint64_t ti0 = DSB_T0();
-				int pass = it < tot ? dsb_map_item(w, &oc, it - opfx, &os, &an) : 0;
+				/* q_buff[-1] is the loop's 0xAA until a push of this call grows the reference's anchor
+				 * vector, which depends on the anchors of every seed before this one: an item after
+				 * the first whose result would change with it sends its seed to the in-order replay */
+				int amb = 0;
+				int pass = it < tot ? dsb_map_item(w, &oc, it - opfx, &os, &an, DSB_QB_M1_LOOP, it > opfx ? &amb : 0) : 0;
 				DSB_T1(DSB_ST_T_MATCH, ti0); /* lane 0: wave clocks in the REF_POS items themselves */
 				uint64_t pm = dsb_gballot<GW>(pass);
+				uint64_t ambm = dsb_gballot<GW>(amb);
 				uint32_t start = opfx > cb ? opfx - cb : 0; /* the owner's first item in this chunk */
 				uint64_t before = (lane == 0 ? 0 : (~0ull >> (64 - lane))) & ~(start == 0 ? 0 : (~0ull >> (64 - start)));
 				uint32_t dest = o_n + (uint32_t)__builtin_popcountll(pm & before);
@@ -1644,6 +1719,8 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 					if (pfx + cnt > cb && lo < hi) {
 						uint64_t mine = (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & ~(lo == 0 ? 0ull : ((1ull << lo) - 1));
 						n_before += (uint32_t)__builtin_popcountll(pm & mine);
+						if (ambm & mine)
+							seed_amb = 1;
 					}
 				}
 			}
@@ -1813,7 +1890,7 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 #endif
 			rec[2 * k] = (pr << 31) | (lane << 24) | a_b;
 			rec[2 * k + 1] = ((uint32_t)(!SLOW && skip && !w->overflow) << 31) | ((uint32_t)(w->overflow != 0) << 30) |
-					 (w->overflow ? 0u : (w->n_anc - a_b));
+					 ((uint32_t)(seed_amb != 0) << 29) | (w->overflow ? 0u : (w->n_anc - a_b));
 		}
 		/* ---- hand the next top seeds to the lanes that finished one, in lane order */
 		uint64_t finm = dsb_gballot<GW>(st == DSB_SM_FIN);
@@ -1888,8 +1965,8 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
 		int act = kk < m;
 		uint32_t cix = act ? tix[kk] : 0;
 		uint32_t r0 = act ? rec[2 * kk] : 0, r1 = act ? rec[2 * kk + 1] : 0;
-		int trig = (int)(r1 >> 31), ovf = (int)((r1 >> 30) & 1);
-		uint32_t cnt = r1 & 0x3fffffffu, src_lane = (r0 >> 24) & 0x7fu, src_off = r0 & 0xffffffu, pool_ = r0 >> 31;
+		int trig = (int)(r1 >> 31), ovf = (int)((r1 >> 29) & 3) != 0; /* overflowed, or replayed for q_buff[-1] */
+		uint32_t cnt = r1 & 0x1fffffffu, src_lane = (r0 >> 24) & 0x7fu, src_off = r0 & 0xffffffu, pool_ = r0 >> 31;
 		uint64_t tm = dsb_gballot<GW>(act && trig);
 		uint64_t om = dsb_gballot<GW>(act && ovf);
 		uint64_t skipm = 0;
@@ -3589,7 +3666,10 @@ DSB_HD int dsb_combine_chain_impl(dsb_read_ws *w, dsb_comb_cache *cc, int chain_
 				int32_t d = 0, q = 0;
 				if (h < w->n_hit) {
 					const dsb_chain_t *c = w->hit + h;
-					ok = c->ref_ID == ref && c->direction == dir && c->sum_score != 0;
+					/* live: not zeroed, and not merged by this speculative run (k_heavy_spec leaves
+					 * its merges in w->hit and only marks them, so the side built second would
+					 * otherwise see a chain the first side already took) */
+					ok = c->ref_ID == ref && c->direction == dir && c->sum_score != 0 && !dsb_spec_merged(w, h);
 					d = isleft ? (int)(c->t_ed - c->q_ed) : (int)(c->t_st - c->q_st);
 					q = isleft ? (int)(c->q_ed - DSB_S_A_KMER_L) : (int)c->q_st;
 				}
@@ -4278,6 +4358,7 @@ DSB_HD void dsb_phase(dsb_read_ws *w, dsb_rflags_t *f, int ph)
 	switch (ph) {
 	case DSB_PH_ISLAND:
 		w->n_anc = 0;
+		w->anc_hw = 0;
 		w->fast_classify = 1;
 		w->n_hit = 0;
 		w->reached_update = 0;
@@ -4306,8 +4387,10 @@ DSB_HD void dsb_phase(dsb_read_ws *w, dsb_rflags_t *f, int ph)
 			if (w->L <= 300 && w->hit[0].sum_score > 200)
 				f->run_slow = 0;
 		}
-		if (f->run_slow)
+		if (f->run_slow) {
+			w->anc_hw = DSB_MAX(w->anc_hw, w->n_anc); /* slow_classify starts at n = 0, the capacity stays */
 			w->n_anc = 0;
+		}
 		return;
 	case DSB_PH_SLOW0:
 		dsb_slow_classify(w, &w->sd[0]);
@@ -4340,7 +4423,7 @@ DSB_HDN void dsb_classify_A(dsb_read_ws *w)
 /* Per-read state carried between phase launches (in the read's workspace). */
 typedef struct {
 	dsb_sdir_t sd[2];
-	uint32_t n_anc, n_hit, fast_classify, overflow, reached_update;
+	uint32_t n_anc, n_hit, fast_classify, overflow, reached_update, anc_hw;
 	dsb_rflags_t f;
 } dsb_rstate_t;
 
@@ -4349,6 +4432,7 @@ DSB_HD void dsb_state_save(const dsb_read_ws *w, const dsb_rflags_t *f, dsb_rsta
 	s->sd[0] = w->sd[0];
 	s->sd[1] = w->sd[1];
 	s->n_anc = w->n_anc;
+	s->anc_hw = w->anc_hw;
 	s->n_hit = w->n_hit;
 	s->fast_classify = w->fast_classify;
 	s->overflow = w->overflow;
@@ -4361,6 +4445,7 @@ DSB_HD void dsb_state_load(dsb_read_ws *w, dsb_rflags_t *f, const dsb_rstate_t *
 	w->sd[0] = s->sd[0];
 	w->sd[1] = s->sd[1];
 	w->n_anc = s->n_anc;
+	w->anc_hw = s->anc_hw;
 	w->n_hit = s->n_hit;
 	w->fast_classify = s->fast_classify;
 	w->overflow = s->overflow;

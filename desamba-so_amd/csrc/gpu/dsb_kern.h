@@ -787,6 +787,9 @@ typedef void (*dsb_phase_fn)(const dsb_dindex_t *, const uint32_t *, const uint6
  * per wave.
  */
 #define DSB_HEAVY_W 16
+/* the DSB_HEAVY_W waves of a read read one read hash: it must be built before them (k_hash_lds), not
+ * by each wave over the shared workspace — k_split sends only reads with dsb_hash_lds_read() here
+ * (none when DSB_HASH_LDS is 0) */
 #define DSB_HEAVY_MAX_HIT 400
 /* launch signatures (kernels.hip takes the kernels from the scoring phase's unit, phase.hip) */
 typedef void (*dsb_heavy_prep_fn)(const dsb_dindex_t *, const uint32_t *, const uint64_t *, const uint32_t *, uint8_t *,

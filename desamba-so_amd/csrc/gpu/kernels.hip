@@ -187,6 +187,7 @@ __global__ __launch_bounds__(256) void k_scatter_u32(uint32_t *__restrict__ dst,
 		dst[idx[i]] = src[i];
 }
 
+#if DSB_TEST_HOOKS /* device self-tests: the test build only (lib/libdesamba_test.so) */
 /* The merge-sort orders the classifier depends on, one array per lane:
  * which 0 chain_cmp_by_pos, 1 chain_cmp_by_MEM_score, 2 chain_cmp_by_score, 3 anchors
  * (Anchor_cmp_by_chr_ID_and_pos), 4 MEM_rst by match_len.  Output: permutation in idx. */
@@ -229,6 +230,7 @@ __global__ void k_selftest_sort(dsb_chain_t *chains, dsb_chain_t *tmp, uint32_t 
 	size_t o = (size_t)t * n;
 	dsb_selftest_one(chains + o, tmp + o, idx + o, tmpi + o, n, which);
 }
+#endif
 
 /* ------------------------------------------------------------------ host side */
 #define DSB_BOUNCE_BYTES ((size_t)32 << 20) /* pinned bounce buffer per context (copy_wait_g) */
@@ -998,7 +1000,9 @@ __global__ __launch_bounds__(64) void k_split(const uint32_t *__restrict__ len, 
 		const dsb_rstate_t *sp = (const dsb_rstate_t *)(ws + ws_off[r] + lay.state);
 		slow = !sp->f.done && !sp->overflow && sp->f.run_slow;
 		uint64_t cost = (!slow && !sp->f.done && !sp->overflow) ? (uint64_t)DSB_MIN(sp->n_hit, 400u) * L : 0;
-		hv = !slow && sp->n_hit && cost >= heavy;
+		/* the heavy reads' waves share the read hash k_hash_lds prebuilt: a read whose hash each
+		 * wave would build itself (dsb_hash_lds_read false) stays in the one-wave scoring */
+		hv = !slow && sp->n_hit && cost >= heavy && dsb_hash_lds_read(L);
 		cls = dsb_cost_class(cost);
 	}
 	uint64_t lt = lane == 0 ? 0 : (~0ull >> (64 - lane));
@@ -2068,6 +2072,7 @@ extern "C" int dsb_gpu_classify(dsb_index *ix, const dsb_reads_t *reads, int *ma
 	return rc;
 }
 
+#if DSB_TEST_HOOKS /* device self-tests: the test build only */
 /* GPU self-test of the glibc-msort restatement: n_arrays x n random keys sorted on the device
  * and on the host with the same code; returns the number of arrays whose permutation differs. */
 extern "C" int dsb_gpu_selftest_sort(uint32_t n, uint32_t n_arrays, int which, uint32_t seed)
@@ -2192,3 +2197,4 @@ extern "C" int dsb_gpu_selftest_occ(const char *dir, uint64_t dollor_pos, const 
 	free(ix);
 	return rc;
 }
+#endif

@@ -74,14 +74,6 @@ int dsb_parse_dump(const char *text, uint64_t text_n, int slow, uint64_t batch_r
 
 const char *dsb_version(void);
 
-/* Self-tests of device code against host code (tests/): the glibc-2.35 msort restatement on the
- * device vs the host (returns the arrays whose permutation differs), and the HBM occ layout of
- * any index's .bwt (rows up to its length, past 2^32 included): out[7 i + c] = occ(rows[i], c) for
- * c = 0..4, out[7 i + 5] = occ(rows[i], 0xff) and out[7 i + 6] the symbol it read (0-4, or 5 for
- * the '$' row, which returns dollor_pos) — reference bwt.c:43-65.  Returns 0, or -1 with err. */
-int dsb_gpu_selftest_sort(uint32_t n, uint32_t n_arrays, int which, uint32_t seed);
-int dsb_gpu_selftest_occ(const char *dir, uint64_t dollor_pos, const uint64_t *rows, uint64_t n, uint64_t *out,
-			 char *err, size_t errn);
 /* sizeof(dsb_timing_t) as this library fills it: a caller built against another version of this
  * header checks it before passing a timing struct (the struct has grown between versions) */
 uint64_t dsb_timing_size(void);

@@ -12,9 +12,9 @@ from conftest import ROOT
 LIB = os.path.join(ROOT, "desamba-so_amd", "lib", "libdesamba.so")
 
 
-def _declared():
+def _declared(headers=("desamba.h", "desamba_mi355x.h")):
     names = set()
-    for h in ("desamba.h", "desamba_mi355x.h"):
+    for h in headers:
         with open(os.path.join(ROOT, "include", h)) as f:
             text = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
         text = re.sub(r"//[^\n]*", "", text)
@@ -86,4 +86,10 @@ def test_test_hooks_only_in_the_test_build():
         assert name.encode() not in prod, name
         assert name.encode() in test, name
     out = subprocess.run(["nm", "-D", "--defined-only", TEST_LIB], capture_output=True, text=True, check=True).stdout
-    assert {l.split()[-1] for l in out.splitlines() if " T " in l} >= _declared()
+    test_exports = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    test_only = _declared(("desamba_mi355x_test.h",))
+    assert {"dsb_gpu_selftest_sort", "dsb_gpu_selftest_occ"} <= test_only
+    assert test_exports == _declared() | test_only, test_exports ^ (_declared() | test_only)
+    # the device self-tests are not in the production library at all
+    assert not (test_only & {l.split()[-1] for l in subprocess.run(
+        ["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout.splitlines() if " T " in l})

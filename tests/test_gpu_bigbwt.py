@@ -7,9 +7,10 @@ way) and queried on the GPU (dsb_gpu_selftest_occ: dsb_occ for c = 0..4 and the 
 at ~1M rows — random rows, rows past 2^32, line / block / superblock edges, the '$' row — each
 compared with the reference's own occ on the same file (oracle/_ref/bigbwt occ, load_bwt + occ,
 src/bwt.c:43-104)."""
-import ctypes as C
+import json
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -53,7 +54,7 @@ def big_bwt(tmp_path_factory):
     yield str(d), dollar
 
 
-def test_occ_past_2_32_rows_matches_reference(big_bwt, pyd, tmp_path):
+def test_occ_past_2_32_rows_matches_reference(big_bwt, tmp_path):
     d, dollar = big_bwt
     rows = rows_to_check(NSYM, dollar)
     assert (rows >= (1 << 32)).sum() > 200_000
@@ -64,14 +65,14 @@ def test_occ_past_2_32_rows_matches_reference(big_bwt, pyd, tmp_path):
                        timeout=900)
     assert r.returncode == 0, r.stderr[-800:]
     want = np.fromfile(op, dtype=np.uint64).reshape(-1, 7)
-    L = pyd.lib()
-    f = L.dsb_gpu_selftest_occ
-    f.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_char_p, C.c_size_t]
-    f.restype = C.c_int
-    got = np.zeros((len(rows), 7), dtype=np.uint64)
-    err = C.create_string_buffer(512)
-    rc = f(d.encode(), DOLLOR_POS, rows.ctypes.data, len(rows), got.ctypes.data, err, 512)
-    assert rc == 0, err.value.decode()
+    # the device occ self-test is in the test build only: run in a process of its own
+    gp = tmp_path / "gpu_occ.bin"
+    w = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "selftest_worker.py"), "occ", d, str(DOLLOR_POS),
+                        str(rp), str(gp)], capture_output=True, text=True, timeout=900)
+    assert w.returncode == 0, w.stderr[-800:]
+    st = json.loads(w.stdout.strip().splitlines()[-1])
+    assert st["rc"] == 0, st["err"]
+    got = np.fromfile(gp, dtype=np.uint64).reshape(-1, 7)
     bad = np.nonzero((got != want).any(axis=1))[0]
     assert len(bad) == 0, [(int(rows[i]), got[i].tolist(), want[i].tolist()) for i in bad[:5]]
     assert int(got[np.nonzero(rows == dollar)[0][0], 6]) == 5  # the '$' row
