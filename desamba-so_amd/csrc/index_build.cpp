@@ -151,6 +151,26 @@ struct Kmers {
 		}
 		return lo;
 	}
+	/* find() of n keys at once: the bucket words, then the keys' search ranges, are prefetched for
+	 * the whole batch before any search runs, so the batch's cache misses overlap instead of
+	 * following one another key by key (the de Bruijn edge pass does one search per position) */
+	void find_batch(const uint64_t *key, uint64_t *loc, int n) const
+	{
+		uint64_t p[64];
+		for (int k = 0; k < n; k++) {
+			p[k] = key[k] >> PRE_MOVE;
+			__builtin_prefetch(&bucket[p[k]]);
+		}
+		for (int k = 0; k < n; k++) {
+			uint64_t lo = bucket[p[k]], hi = bucket[p[k] + 1];
+			__builtin_prefetch(&v[lo]);
+			__builtin_prefetch(&v[lo + ((hi - lo) >> 1)]);
+			if (hi > lo)
+				__builtin_prefetch(&v[hi - 1]);
+		}
+		for (int k = 0; k < n; k++)
+			loc[k] = find(key[k]);
+	}
 };
 
 /* ------------------------------------------------------------------ reference */
@@ -299,6 +319,30 @@ void build_edges(const Ref &ref, Kmers &km, std::vector<uint64_t> &heads, std::v
 				run = 0;
 			}
 		}
+		/* positions are searched in batches of NB (km.find_batch), then applied in order */
+		constexpr int NB = 32;
+		uint64_t bkey[NB], bloc[NB], bpos[NB];
+		int nb = 0;
+		auto flush = [&] {
+			km.find_batch(bkey, bloc, nb);
+			for (int q = 0; q < nb; q++) {
+				uint64_t j = bpos[q], loc = bloc[q];
+				bool first = !(j > 0 && BIT[s[j - 1]] < 4);
+				bool last = !acgt(j + K);
+				uint16_t e = 0;
+				if (!first)
+					e |= (uint16_t)(1u << (BIT[s[j - 1]] + 4));
+				if (!last)
+					e |= (uint16_t)(1u << BIT[s[j + K]]);
+				if (e)
+					or16(info + loc, e);
+				if (first)
+					th[ti].push_back(loc);
+				if (last)
+					tt[ti].push_back(loc);
+			}
+			nb = 0;
+		};
 		for (uint64_t j = j0; j < t.hi; j++) {
 			uint64_t p = j + K - 1;
 			if (p >= L)
@@ -312,21 +356,12 @@ void build_edges(const Ref &ref, Kmers &km, std::vector<uint64_t> &heads, std::v
 			}
 			if (run < K)
 				continue;
-			uint64_t loc = km.find(key);
-			bool first = !(j > 0 && BIT[s[j - 1]] < 4);
-			bool last = !acgt(j + K);
-			uint16_t e = 0;
-			if (!first)
-				e |= (uint16_t)(1u << (BIT[s[j - 1]] + 4));
-			if (!last)
-				e |= (uint16_t)(1u << BIT[s[j + K]]);
-			if (e)
-				or16(info + loc, e);
-			if (first)
-				th[ti].push_back(loc);
-			if (last)
-				tt[ti].push_back(loc);
+			bkey[nb] = key;
+			bpos[nb] = j;
+			if (++nb == NB)
+				flush();
 		}
+		flush();
 	});
 	for (auto &v : th) heads.insert(heads.end(), v.begin(), v.end());
 	for (auto &v : tt) tails.insert(tails.end(), v.begin(), v.end());
@@ -423,6 +458,97 @@ void walk_unitigs(Kmers &km, uint64_t n_uni, Unitigs &u)
 			}
 			p.end.push_back(v[loc]);
 			last = (uint16_t)(4u << 10);
+			p.len.push_back(L);
+			p.start.push_back(v[i]);
+		}
+	});
+	for (auto &p : part) {
+		u.len.insert(u.len.end(), p.len.begin(), p.len.end());
+		u.start.insert(u.start.end(), p.start.begin(), p.start.end());
+		u.end.insert(u.end.end(), p.end.begin(), p.end.end());
+	}
+	if (u.len.size() != n_uni)
+		die("unitig count differs from the number of end k-mers");
+}
+
+/* The same walks without a search per step.
+ *
+ * Successors: a k-mer x that is not an end has exactly one out edge c, and its successor is
+ * ((x & MASK60) << 2) | c.  The k-mers with one first base are a contiguous range of the sorted
+ * list, and over such a range that key increases with the index, so every successor of a slice of
+ * the list is found by one forward merge over the list (nx[i], sequential reads) instead of a
+ * bucketed binary search per walk step (several dependent cache misses each: 80 of the 182 s of
+ * the c2l18 build, 179 of 470 s for c2xl, in the range form above).
+ *
+ * Preceding characters: the walk ORs into every k-mer after a unitig's first the first base of
+ * the k-mer it came from.  A successor y of a non-end x has exactly one in edge (setLabel marks x
+ * an end when y has in != 1 or is a sequence head, idx.c:392-489), and that edge's character is
+ * x's first base; so a walk step reads only nx[] and y's flags.  Unitig starts take '#', except the
+ * first start of the whole list, which the reference's range 0 gives '$' (idx.c:741-745).
+ *
+ * Unitig ids follow the start k-mers' order in the list in both forms (the ranges are contiguous
+ * and walked in order), so the starts are handed out in slices and the slices concatenated. */
+template <class IX> void walk_unitigs_nx(Kmers &km, uint64_t n_uni, Unitigs &u)
+{
+	uint16_t *info = km.info.data();
+	const uint64_t *v = km.v.data();
+	const uint64_t n = km.n;
+	std::vector<IX> nx(n);
+	constexpr uint64_t SLICE = 1 << 22;
+	const uint64_t n_sl = (n + SLICE - 1) / SLICE;
+	par_tasks(n_sl, g_threads, [&](uint64_t s) {
+		uint64_t lo = s * SLICE, hi = std::min(n, lo + SLICE), j = 0;
+		int grp = -1;
+		for (uint64_t i = lo; i < hi; i++) {
+			uint16_t x = ld16(info + i);
+			if (x & F_END)
+				continue;
+			unsigned c = (unsigned)__builtin_ctz(x & 15u);
+			if ((x & 15u) == 0)
+				die("unitig walk reached a k-mer without an out edge");
+			uint64_t key = ((v[i] & MASK60) << 2) | c;
+			int b = (int)(v[i] >> ((K - 1) * 2));
+			if (b != grp) { /* a new first-base range: the merge restarts at a search */
+				grp = b;
+				j = (uint64_t)(std::lower_bound(v, v + n, key) - v);
+			}
+			while (j < n && v[j] < key)
+				j++;
+			if (j == n || v[j] != key) {
+				char t[40];
+				snprintf(t, sizeof t, "%016llx", (unsigned long long)key);
+				die("a successor 31-mer is missing from the k-mer list: ", t);
+			}
+			nx[i] = (IX)j;
+		}
+	});
+	uint64_t first_start = n;
+	for (uint64_t i = 0; i < n; i++)
+		if (ld16(info + i) & F_START) {
+			first_start = i;
+			break;
+		}
+	std::vector<Unitigs> part(n_sl);
+	par_tasks(n_sl, g_threads, [&](uint64_t s) {
+		uint64_t lo = s * SLICE, hi = std::min(n, lo + SLICE);
+		Unitigs &p = part[s];
+		for (uint64_t i = lo; i < hi; i++) {
+			if (!(ld16(info + i) & F_START))
+				continue;
+			or16(info + i, (uint16_t)((i == first_start ? 5u : 4u) << 10));
+			uint64_t loc = i;
+			uint32_t L = K;
+			uint16_t x = ld16(info + loc);
+			while (!(x & F_END)) {
+				loc = nx[loc];
+				x = ld16(info + loc);
+				unsigned in = (x >> 4) & 15u;
+				if (popc4(in) != 1)
+					die("unitig walk: a successor without exactly one in edge");
+				or16(info + loc, (uint16_t)((unsigned)__builtin_ctz(in) << 10));
+				L++;
+			}
+			p.end.push_back(v[loc]);
 			p.len.push_back(L);
 			p.start.push_back(v[i]);
 		}
@@ -1153,7 +1279,15 @@ int main(int argc, char **argv)
 	uint64_t n_uni = set_labels(km, heads, tails);
 	note("unitig labels");
 	Unitigs u;
-	walk_unitigs(km, n_uni, u);
+	{
+		const char *rw = getenv("DSB_INDEX_RANGE_WALK"); /* the reference's 16 ranges with a search per step */
+		if (rw && *rw == '1')
+			walk_unitigs(km, n_uni, u);
+		else if (km.n < (1ull << 32))
+			walk_unitigs_nx<uint32_t>(km, n_uni, u);
+		else
+			walk_unitigs_nx<uint64_t>(km, n_uni, u);
+	}
 	note("unitigs");
 	std::vector<UnitigRec> uv;
 	std::vector<RefUni> ru;
