@@ -609,7 +609,23 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_spset_t *s) { return dsb_spset_inse
 #define DSB_HSET_POOL 0
 #endif
 #endif
-typedef struct { uint64_t *tab; uint32_t stride, gen; int l, m; uint64_t tag; } dsb_hset_t;
+/* The first DSB_HSET_L1_MAX entries of a generation go to a small per-lane table in LDS
+ * (DSB_HSET_L1 slots of 8 bytes, (generation & 0xffffff) << 40 | node; BWT rows are < 2^40,
+ * checked at index load), and only the entries after them to the pool set.  A lookup probes the
+ * LDS table first, so membership is unchanged.  Measured with the emulator on C2-proxy ONT reads
+ * (tests/emu emu_prof, INSHIST): 81% of all inserts happen while the set holds fewer than 24
+ * entries, 91% below 32 — those never touch HBM, where each insert was a dependent 16-B probe and a
+ * scattered store (the fast seeding's WRITE_SIZE).  lt == 0: no first level (the host paths). */
+#ifndef DSB_HSET_L1_LOG2
+#define DSB_HSET_L1_LOG2 5
+#endif
+#define DSB_HSET_L1 (1u << DSB_HSET_L1_LOG2)
+#ifndef DSB_HSET_L1_MAX
+#define DSB_HSET_L1_MAX 24 /* < DSB_HSET_L1: a probe always meets a free slot */
+#endif
+static_assert(DSB_HSET_L1_MAX < DSB_HSET_L1, "first-level sp_set table");
+#define DSB_HSET_NODE_BITS 40
+typedef struct { uint64_t *tab; uint32_t stride, gen; int l, m; uint64_t tag; uint64_t *lt; } dsb_hset_t;
 /* slot tag without the pool: the launch's tag (a host counter bumped for every phase launch, so
  * two launches — FAST0/FAST1, SLOW0/SLOW1, later chunks reusing the same workspace bytes, overflow
  * re-runs — never share one) in the high word, the lane's generation in the low word */
@@ -618,10 +634,15 @@ DSB_HD uint64_t dsb_hset_tag(const dsb_read_ws *w)
 	return w->launch_tag << DSB_HSET_GEN_BITS;
 }
 /* the set of this lane: `hset` holds the wave's DSB_WV interleaved tables; slot tags are `tag` +
- * the lane's generation (generation 0 is never used: every seed resets the set first) */
-DSB_HD dsb_hset_t dsb_hset_make(uint64_t *hset, uint64_t tag)
+ * the lane's generation (generation 0 is never used: every seed resets the set first).  `lt`: the
+ * wave's first-level LDS tables (DSB_HSET_L1 x DSB_WV u64, lane-interleaved) or 0; this lane's
+ * slots are cleared to generation 0 here (LDS starts undefined in every workgroup). */
+DSB_HD dsb_hset_t dsb_hset_make(uint64_t *hset, uint64_t tag, uint64_t *lt)
 {
-	dsb_hset_t hs = {hset + DSB_HSET_SLOT_U64 * dsb_lane(), DSB_HSET_SLOT_U64 * DSB_WV, 0, 0, 500, tag};
+	dsb_hset_t hs = {hset + DSB_HSET_SLOT_U64 * dsb_lane(), DSB_HSET_SLOT_U64 * DSB_WV, 0, 0, 500, tag, lt ? lt + dsb_lane() : 0};
+	if (hs.lt)
+		for (int k = 0; k < DSB_HSET_L1; k++)
+			hs.lt[(uint32_t)k * DSB_WV] = 0;
 	return hs;
 }
 DSB_HD void dsb_set_reset(dsb_hset_t *s)
@@ -637,6 +658,27 @@ DSB_HD int dsb_set_insert(uint64_t node, dsb_hset_t *s)
 	if (s->l == s->m) {
 		s->l = 0;
 		s->gen++;
+	}
+#ifdef DSB_EMU_PROF
+	dsb_emu_prof_insert(s->l);
+#endif
+	if (s->lt) { /* first level: the generation's first DSB_HSET_L1_MAX entries */
+		uint64_t g24 = (uint64_t)(s->gen & ((1u << DSB_HSET_GEN_BITS) - 1));
+		uint64_t want = (g24 << DSB_HSET_NODE_BITS) | node;
+		uint32_t h = (uint32_t)((node * 0x9E3779B97F4A7C15ull) >> (64 - DSB_HSET_L1_LOG2));
+		for (;;) {
+			uint64_t e = s->lt[h * DSB_WV];
+			if (e == want)
+				return 0;
+			if ((e >> DSB_HSET_NODE_BITS) != g24)
+				break; /* a free slot: the node is not in the first level */
+			h = (h + 1) & (DSB_HSET_L1 - 1);
+		}
+		if (s->l < DSB_HSET_L1_MAX) {
+			s->lt[h * DSB_WV] = want;
+			s->l++;
+			return 1;
+		}
 	}
 	uint32_t h = (uint32_t)((node * 0x9E3779B97F4A7C15ull) >> (64 - DSB_HSET_LOG2));
 	uint64_t g = s->tag + (s->gen & ((1u << DSB_HSET_GEN_BITS) - 1));
@@ -2049,17 +2091,18 @@ DSB_HDN void dsb_seed_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, dsb_hset_t *hsp,
  * `tag` on (dsb_hset_make).  Returns the lane's last generation: the wave's maximum + 1 is the
  * next free tag offset of these tables. */
 template <int G = 64>
-DSB_HDN uint32_t dsb_fast_classify_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, uint64_t tag, int32_t *lds)
+DSB_HDN uint32_t dsb_fast_classify_sm(dsb_read_ws *w, const dsb_sdir_t *s_d, uint64_t *hset, uint64_t tag, int32_t *lds,
+				      uint64_t *lt = 0)
 {
-	dsb_hset_t hs = dsb_hset_make(hset, tag);
+	dsb_hset_t hs = dsb_hset_make(hset, tag, lt);
 	dsb_seed_sm<false, G>(w, s_d, &hs, w->mem, lds);
 	return hs.gen;
 }
 template <int G = 64>
 DSB_HDN uint32_t dsb_slow_classify_sm(dsb_read_ws *w, const dsb_sdir_t *sd, uint64_t *hset, uint64_t tag, dsb_mem_t *memtmp,
-				      int32_t *lds)
+				      int32_t *lds, uint64_t *lt = 0)
 {
-	dsb_hset_t hs = dsb_hset_make(hset, tag);
+	dsb_hset_t hs = dsb_hset_make(hset, tag, lt);
 	dsb_seed_sm<true, G>(w, sd, &hs, memtmp, lds);
 	return hs.gen;
 }

@@ -578,6 +578,11 @@ __device__ __forceinline__ void dsb_hpool_release(const dsb_dindex_t *ix, uint32
 }
 #endif
 
+/* the seeding sp_set's first level in LDS (dsb_classify.h dsb_set_insert); 0: every entry in the pool set */
+#ifndef DSB_HSET_LDS
+#define DSB_HSET_LDS 1
+#endif
+
 /* Lanes per read of the seeding phases (FAST0/1, SLOW0/1): 64 = a wave per read; 32 = two reads
  * per wave, each on a half-wave group running the state machine of dsb_seed_sm on its own (a
  * read's wave time is set by its longest seed, so the other lanes mostly wait: tools/seed_prof). */
@@ -666,14 +671,15 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 			uint32_t last_gen;
 #endif
 			/* LDS: per group, 2 x G ints (dsb_seed_sm's owner / max arrays) */
+			/* the sp_set's first level (dsb_set_insert): DSB_HSET_L1 u64 per lane, 16 KB per wave */
+			__shared__ uint64_t hs_l1[DSB_HSET_LDS ? DSB_HSET_L1 * 64 : 1];
 			if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
 				__shared__ int32_t sm_lds[2 * 64];
-				__shared__ uint8_t hb_lds_f[DSB_HB_LDS];
-				w.lds_hb = hb_lds_f;
-				last_gen = dsb_fast_classify_sm<G>(&w, &w.sd[ph - DSB_PH_FAST0], hset, hs_tag, sm_lds);
+				last_gen = dsb_fast_classify_sm<G>(&w, &w.sd[ph - DSB_PH_FAST0], hset, hs_tag, sm_lds, DSB_HSET_LDS ? hs_l1 : nullptr);
 			} else {
 				__shared__ int32_t sm_lds2[2 * 64];
-				last_gen = dsb_slow_classify_sm<G>(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, hs_tag, w.mem, sm_lds2);
+				last_gen = dsb_slow_classify_sm<G>(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, hs_tag, w.mem, sm_lds2,
+								   DSB_HSET_LDS ? hs_l1 : nullptr);
 			}
 #if !DSB_HSET_POOL
 			(void)last_gen;

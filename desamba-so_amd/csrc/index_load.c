@@ -247,6 +247,10 @@ int dsb_index_load_bwt(dsb_index *ix, const char *dir, int with_hash, char *err,
 	FILE *f;
 	if (!(f = open_ix(dir, ".bwt", err, errn))) return -1;
 	if (rd(f, &ix->byteLen, 8, 1, "bwt len", err, errn)) goto fail;
+	if (ix->byteLen / 168 >= (1ull << 32)) { /* 256 rows per 168-B block: rows < 2^40 (the seeding's packed sp_set slots) */
+		snprintf(err, errn, "BWT of %llu bytes: more than 2^40 rows", (unsigned long long)ix->byteLen);
+		goto fail;
+	}
 	ix->bwt_occ = xm(ix->byteLen + 256); /* slack: occ may touch the u16 after a block */
 	memset(ix->bwt_occ + ix->byteLen, 0xFF, 256);
 	if (rd(f, ix->bwt_occ, 1, ix->byteLen, "bwt occ", err, errn)) goto fail;

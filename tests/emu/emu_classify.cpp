@@ -21,6 +21,9 @@ static void dsb_emu_prof_seed(int slow, uint32_t k, uint64_t trips, uint64_t map
 {
 	g_prof[slow ? 1 : 0].push_back({k, trips, maps});
 }
+/* sp_set inserts by the set's fill at the time (l = entries since the last reset / wrap) */
+static uint64_t g_ins_hist[512];
+static void dsb_emu_prof_insert(int l) { g_ins_hist[l < 512 ? l : 511]++; }
 #endif
 extern "C" {
 #include "../../desamba-so_amd/csrc/dsb_host.h"
@@ -118,13 +121,18 @@ int main(int argc, char **argv)
 				static std::vector<uint64_t> hset_store(DSB_HSET_WAVE_U64, 0);
 				static uint64_t gen_base = 0;
 				uint64_t *hset = hset_store.data();
+				/* the first-level table in LDS (garbage at workgroup start; dsb_hset_make clears it);
+				 * EMU_HSET_L1=0: none, every entry in the pool set */
+				static uint64_t hs_l1_store[DSB_HSET_L1];
+				memset(hs_l1_store, 0xA7, sizeof(hs_l1_store));
+				uint64_t *hs_l1 = (getenv("EMU_HSET_L1") && !atoi(getenv("EMU_HSET_L1"))) ? nullptr : hs_l1_store;
 				for (int ph = 0; ph < DSB_PH_DELA; ph++) {
 					if ((ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) && dsb_phase_active(&w, &f, ph)) {
 						static int32_t sm_lds[2];
-						gen_base += dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, gen_base, sm_lds) + 1;
+						gen_base += dsb_fast_classify_sm(&w, &w.sd[ph - DSB_PH_FAST0], hset, gen_base, sm_lds, hs_l1) + 1;
 					} else if ((ph == DSB_PH_SLOW0 || ph == DSB_PH_SLOW1) && dsb_phase_active(&w, &f, ph)) {
 						static int32_t sm_lds2[2];
-						gen_base += dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, gen_base, w.mem, sm_lds2) + 1;
+						gen_base += dsb_slow_classify_sm(&w, &w.sd[ph == DSB_PH_SLOW0 ? 0 : 1], hset, gen_base, w.mem, sm_lds2, hs_l1) + 1;
 					} else if (ph == DSB_PH_RESOLVE_F || ph == DSB_PH_RESOLVE_S0 || ph == DSB_PH_RESOLVE_S1) {
 						/* the resolve kernels' LDS sort / M3 staging arrays (garbage between reads) */
 						static uint64_t lds_key[DSB_SORT_LDS_SLOW];
@@ -145,7 +153,7 @@ int main(int argc, char **argv)
 				dsb_classify_A(&w);
 #ifdef DSB_EMU_PROF
 			if (scale == DSB_SCALE_UNIT) {
-				printf("R %lu %u", (unsigned long)i, L);
+				printf("R %lu %u A %u %u", (unsigned long)i, L, (unsigned)w.n_anc, (unsigned)w.fast_classify);
 				for (int sl = 0; sl < 2; sl++) {
 					printf(" %s", sl ? "|S" : "|F");
 					for (const emu_prof_seed &q : g_prof[sl]) printf(" %lu,%lu", (unsigned long)q.trips, (unsigned long)q.maps);
@@ -175,6 +183,11 @@ int main(int argc, char **argv)
 		}
 	}
 	fwrite(out.s, 1, out.l, stdout);
+#ifdef DSB_EMU_PROF
+	printf("INSHIST");
+	for (int k = 0; k < 512; k++) printf(" %lu", (unsigned long)g_ins_hist[k]);
+	printf("\n");
+#endif
 	if (stats) {
 		fprintf(stderr, "reads %lu retries %lu\n", (unsigned long)reads.n, (unsigned long)n_retry);
 		const char *nm[DSB_ST_N] = {"occ", "occ_nib", "memsearch", "sa", "uni", "refpos", "getref_b", "anchor", "chain", "ek1", "ek2", "hash_b", "lookup", "node", "t_mem", "t_map"};

@@ -21,7 +21,7 @@ def parse(paths):
                 continue
             head, rest = line.split("|F")
             fpart, spart = rest.split("|S")
-            _, i, L = head.split()
+            _, i, L = head.split()[:3]
             f = [tuple(map(int, x.split(","))) for x in fpart.split()]
             s = [tuple(map(int, x.split(","))) for x in spart.split()]
             yield int(i), int(L), f, s
