@@ -124,6 +124,7 @@ __global__ __launch_bounds__(64, DSB_MINW_LANE) void k_island(const dsb_dindex_t
 	dsb_rstate_t *sp = (dsb_rstate_t *)(base + dsb_layout(L, cap).state);
 	dsb_rflags_t f = {0, 0, 0, 0};
 	w.n_anc = 0;
+	w.anc_hw = 0;
 	w.fast_classify = 1;
 	w.n_hit = 0;
 	w.reached_update = 0;
@@ -357,6 +358,7 @@ __global__ __launch_bounds__(64, DSB_MINW_ISLAND) void k_island_g(const dsb_dind
 		sp->sd[0] = a;
 		sp->sd[1] = c;
 		sp->n_anc = 0;
+		sp->anc_hw = 0; /* the read's anchor-vector high-water mark (dsb_map_seed): the workspace holds an earlier read's */
 		sp->n_hit = 0;
 		sp->fast_classify = 1;
 		sp->overflow = 0;

@@ -90,6 +90,7 @@ DSB_HD void dsb_ws_init(dsb_read_ws *w, const dsb_dindex_t *ix, uint8_t *base, u
 	w->seeds = (dsb_seed_t *)(base + o.seeds);
 	w->anc = (dsb_anchor_t *)(base + o.anc);
 	w->n_anc = 0;
+	w->anc_hw = 0;
 	w->anc_tmp = (dsb_anchor_t *)(base + o.anc_tmp);
 	w->anc_tmp2 = (dsb_anchor_t *)(base + o.anc_tmp2);
 	w->sidx = (uint32_t *)(base + o.sidx);

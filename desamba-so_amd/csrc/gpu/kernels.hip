@@ -1324,6 +1324,13 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		if (const char *e = getenv("DSB_TEST_SCALE0"))
 			scale0 = (uint32_t)DSB_MAX(1, atoi(e));
 	std::vector<uint32_t> scale(n, scale0);
+	/* DSB_TEST_WS_FILL=b (test build only): the chunk workspace and the re-run reads' bytes are filled
+	 * with byte b before the kernels run, so that a per-read field the kernels read before writing
+	 * shows up (workspace bytes are otherwise an earlier read's, or zero in a fresh allocation) */
+	int ws_fill = -1;
+	if (DSB_TEST_HOOKS)
+		if (const char *e = getenv("DSB_TEST_WS_FILL"))
+			ws_fill = (int)(strtol(e, NULL, 0) & 0xff);
 	/* DSB_TEST_FORCE_RERUN=k (test build only): every k-th read re-runs as if it had overflowed */
 	uint64_t force_rerun = 0;
 	if (DSB_TEST_HOOKS)
@@ -1346,7 +1353,9 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	 * are cl[i] / cso[i]: one chunk, or the deferred overflows of the whole batch (below) */
 	auto retry_view = [&](uint32_t cn, uint64_t cb, const std::vector<uint32_t> &vlen, std::vector<uint32_t> &vscale,
 			      std::vector<uint64_t> &vws_off, std::vector<dsb_read_out_t> &vro, const uint32_t *cl,
-			      const uint64_t *cso, uint8_t *wsb, uint64_t &rused, uint32_t n_over) -> int {
+			      const uint64_t *cso, uint8_t *wsb, uint64_t &rused, uint32_t n_over, const uint32_t *vid) -> int {
+		/* the batch's read number of view entry i (vid: the deferred re-runs' map) */
+		auto rid = [&](uint32_t i) -> unsigned long { return vid ? (unsigned long)vid[i] : (unsigned long)(cb + i); };
 		while (n_over) {
 			std::vector<uint32_t> sel;
 			for (uint32_t i = 0; i < cn; i++)
@@ -1355,13 +1364,14 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			if (host_timing())
 				for (uint32_t i : sel)
 					fprintf(stderr, "[dsb retry] read %lu L %u scale %u status %#x anchors %u hits %u\n",
-						(unsigned long)(cb + i), vlen[cb + i], vscale[cb + i], vro[cb + i].status,
+						rid(i), vlen[cb + i], vscale[cb + i], vro[cb + i].status,
 						vro[cb + i].n_anchor, vro[cb + i].n_hit);
 			uint64_t tot2 = 0;
 			for (uint32_t i : sel) {
 				vscale[cb + i] *= DSB_CAP_RETRY;
 				if (vscale[cb + i] > 4096 * DSB_SCALE_UNIT) {
-					snprintf(err, errn, "read %lu overflows every workspace size", (unsigned long)(cb + i));
+					snprintf(err, errn, "read %lu (length %u) overflows every workspace size (status %#x, %u anchors, %u hits)",
+						 rid(i), vlen[cb + i], vro[cb + i].status, vro[cb + i].n_anchor, vro[cb + i].n_hit);
 					return -1;
 				}
 				vws_off[cb + i] = tot2; /* within this round's part of the retry buffer (rebased below) */
@@ -1406,6 +1416,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				uint64_t rbase = (uint64_t)(uintptr_t)g->wsr.p - (uint64_t)(uintptr_t)wsb + rused;
 				for (uint32_t i : sel)
 					vws_off[cb + i] += rbase;
+				if (ws_fill >= 0) /* tests: the re-run reads' bytes as an earlier read's leftovers */
+					HIP_OK(hipMemsetAsync((uint8_t *)g->wsr.p + rused, ws_fill, tot2, s));
 				rused += tot2;
 			}
 			HIP_OK(copy_wait_g(g, g->ws_off.p, vws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
@@ -1489,6 +1501,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		}
 		if (g->order.ensure(4 * (size_t)cn + 4, err, errn) || g->word_off.ensure(8 * (size_t)cn + 16, err, errn))
 			return -1;
+		if (ws_fill >= 0) /* tests: every read's workspace starts as another read's leftovers would */
+			HIP_OK(hipMemsetAsync(WS.p, ws_fill, ws_total, s));
 		if (!DSB_HSET_POOL && WS.p != ws_before) /* fresh bytes: no stale sp_set slot may carry a live tag */
 			HIP_OK(hipMemsetAsync(WS.p, 0, WS.cap, s));
 		HIP_OK(copy_wait_g(g, g->ws_off.p, ws_off.data() + cb, 8ull * cn, hipMemcpyHostToDevice, s));
@@ -1580,7 +1594,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				n_over = 0;
 			}
 		}
-		if (n_over && retry_view(cn, cb, len, scale, ws_off, h_ro, cl, cso, wsb, rused, n_over))
+		if (n_over && retry_view(cn, cb, len, scale, ws_off, h_ro, cl, cso, wsb, rused, n_over, nullptr))
 			return -1;
 		hs_mark(HS_RETRY);
 		if (getenv("DSB_DEBUG_READ")) { /* diagnostic: dump one read's workspace after stage A */
@@ -1717,7 +1731,7 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		 * workspace was released */
 		uint8_t *wsb = WS.p ? WS.as<uint8_t>() : (uint8_t *)g->wsr.p;
 		const uint32_t *vcl = g->vlen.as<uint32_t>();
-		if (retry_view(m, 0, vlen, vscale, vws, vro, vcl, g->vso.as<uint64_t>(), wsb, rused, m))
+		if (retry_view(m, 0, vlen, vscale, vws, vro, vcl, g->vso.as<uint64_t>(), wsb, rused, m, vidx.data()))
 			return -1;
 		std::vector<uint32_t> vord(m);
 		uint64_t worst = 0;

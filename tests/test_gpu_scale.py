@@ -325,6 +325,31 @@ def test_c2_lek18_qbuff_byte_read_set(pyd, tmp_path):
     _check_vs_reference(pyd, d, fq, 49921, "C2-lek18-divergence")
 
 
+def test_c2_lek18_qbuff_byte_with_dirty_workspace(tmp_path):
+    """The same read set with every read's workspace filled with 0x5A before the kernels run
+    (DSB_TEST_WS_FILL, test library), alone and with every seed group replayed in order
+    (DSB_WAVE_DBG=32, so every map_seed is the sequential one, which reads the per-read anchor-vector
+    high-water mark).  Round 6 found that field left uninitialised by the island kernel: fresh
+    workspaces read 0 and passed, but in a 1M-read c2l18 batch the re-run reads met an earlier read's
+    bytes there and four of them ended in M3's NULL case (status 8).  Byte-identical to the clean run
+    and to the hermetic reference."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import proxy_build
+    from test_gpu_hooks import run_worker
+    _need(proxy_build.BUILDER)
+    avail = _host_bytes_available()
+    if avail is not None and avail < (96 << 30):
+        pytest.skip(f"host memory short for the c2l18 build: {avail >> 30} GiB available")
+    d = os.environ.get("DSB_C2L18_DIR") or proxy_build.ensure_proxy("c2l18")
+    fq = _sim(d, tmp_path, 1000, 49921, "ont")
+    _need(HERM)
+    herm = subprocess.run([HERM, "--sam", d, str(fq)], capture_output=True, check=True, timeout=900).stdout
+    for env in ({"DSB_TEST_WS_FILL": "0x5A"}, {"DSB_TEST_WS_FILL": "0x5A", "DSB_WAVE_DBG": "32"}):
+        outs, _ = run_worker(tmp_path, "fill" + env.get("DSB_WAVE_DBG", ""), d, [fq], env)
+        bad = [a[0] for a, b in zip(groups(herm), groups(outs[0])) if a != b]
+        assert not bad, (env, bad[:5])
+
+
 @pytest.mark.timeout(1150)  # the build alone takes 8-10 min on the box's 16 cores
 def test_c2xl_proxy_past_2_32_rows_matches_reference(pyd, tmp_path):
     """The C2 scale: tools/simulate.py preset c2xl (~5 Gbp, ~2.8 G distinct 31-mers, 2 GB e-kmer
