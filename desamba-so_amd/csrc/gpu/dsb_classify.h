@@ -848,7 +848,9 @@ DSB_HD void dsb_get_ref_r(dsb_read_ws *w, dsb_w32 &T, uint64_t uni_offset, uint3
  * DSB_QB_FIRST_PUSH is what the first push leaves.
  */
 #define DSB_QB_M1_LOOP 0xAA /* q_buff[-1] before any push of the call grew the anchor vector */
+#ifndef DSB_QB_M1_GROWN /* (tools: -DDSB_QB_M1_GROWN=0xAA builds the model without the realloc byte) */
 #define DSB_QB_M1_GROWN 0x00 /* after one did */
+#endif
 #ifndef DSB_QB_FIRST_PUSH
 #define DSB_QB_FIRST_PUSH DSB_QB_M1_GROWN
 #endif

@@ -682,27 +682,57 @@ inline int sp_cmp(const SpK &a, const SpK &b)
 }
 
 /* one pass of ksort_stable_step (utils.c:396-461): runs of `w` elements merged pairwise,
- * the left element taken when cmp(left, right) >= 0, a trailing lone run copied */
+ * the left element taken when cmp(left, right) >= 0, a trailing lone run copied.
+ *
+ * spkmer_cmp_l orders the strings "the last sp_pos bases of the k-mer, then '#'" lexicographically
+ * with '#' below every base (cmp 1: a before b, -1: after, 0: the same string), a total preorder,
+ * so "cmp(left, right) >= 0" is the stable merge rule and the merge path can be cut anywhere: the
+ * last levels (a few huge merges, one thread each in the reference's schedule) are split into
+ * segments at merge-path points found by binary search (the smallest i on output diagonal k with
+ * B[k-i-1] before A[i]) and the segments merged in parallel — the same output element by element.
+ * DSB_INDEX_SERIAL_MERGE=1 merges each pair on one thread (the check). */
 void merge_pass(const SpK *from, SpK *to, uint64_t n, uint64_t w, int nt)
 {
 	uint64_t pairs = 0;
 	for (uint64_t b = 0; b + w < n; b += 2 * w) pairs++;
-	auto merge_one = [&](uint64_t k) {
-		uint64_t b1 = k * 2 * w, e1 = b1 + w, b2 = e1, e2 = std::min(b2 + w, n);
-		uint64_t p1 = b1, p2 = b2, p = b1;
-		while (p1 < e1 && p2 < e2) {
-			if (sp_cmp(from[p1], from[p2]) >= 0)
-				to[p++] = from[p1++];
+	auto merge_seg = [&](const SpK *a, uint64_t na, const SpK *b, uint64_t nb, SpK *o) {
+		uint64_t p1 = 0, p2 = 0, p = 0;
+		while (p1 < na && p2 < nb) {
+			if (sp_cmp(a[p1], b[p2]) >= 0)
+				o[p++] = a[p1++];
 			else
-				to[p++] = from[p2++];
+				o[p++] = b[p2++];
 		}
-		while (p1 < e1) to[p++] = from[p1++];
-		while (p2 < e2) to[p++] = from[p2++];
+		while (p1 < na) o[p++] = a[p1++];
+		while (p2 < nb) o[p++] = b[p2++];
 	};
-	if (pairs > 64 && nt > 1)
-		par_tasks(pairs, nt, merge_one);
+	/* elements of A among the first k outputs of merging A and B */
+	auto split = [&](const SpK *a, uint64_t na, const SpK *b, uint64_t nb, uint64_t k) -> uint64_t {
+		uint64_t lo = k > nb ? k - nb : 0, hi = std::min(k, na);
+		while (lo < hi) {
+			uint64_t mid = lo + ((hi - lo) >> 1);
+			if (sp_cmp(a[mid], b[k - mid - 1]) < 0) /* B[k-mid-1] goes before A[mid] */
+				hi = mid;
+			else
+				lo = mid + 1;
+		}
+		return lo;
+	};
+	const char *ser = getenv("DSB_INDEX_SERIAL_MERGE");
+	uint64_t segs = (nt > 1 && pairs < (uint64_t)nt * 4 && !(ser && *ser == '1')) ? ((uint64_t)nt * 8 + pairs - 1) / pairs : 1;
+	auto one = [&](uint64_t q) {
+		uint64_t k = q / segs, sg = q % segs;
+		uint64_t b1 = k * 2 * w, e1 = b1 + w, b2 = e1, e2 = std::min(b2 + w, n);
+		const SpK *A = from + b1, *B = from + b2;
+		uint64_t na = e1 - b1, nb = e2 - b2, tot = na + nb;
+		uint64_t k0 = tot * sg / segs, k1 = tot * (sg + 1) / segs;
+		uint64_t i0 = split(A, na, B, nb, k0), i1 = split(A, na, B, nb, k1);
+		merge_seg(A + i0, i1 - i0, B + (k0 - i0), (k1 - i1) - (k0 - i0), to + b1 + k0);
+	};
+	if (nt > 1 && pairs * segs > 1)
+		par_tasks(pairs * segs, nt, one);
 	else
-		for (uint64_t k = 0; k < pairs; k++) merge_one(k);
+		for (uint64_t q = 0; q < pairs * segs; q++) one(q);
 	uint64_t b = pairs * 2 * w;
 	if (b < n)
 		memcpy(to + b, from + b, (n - b) * sizeof(SpK));
@@ -982,35 +1012,63 @@ void sa_walk_par(const Bwt &bw, const Rank &rk, const std::vector<UnitigRec> &uv
 	}
 	if (st[n] != bw.len)
 		die("unitig lengths do not add up to the BWT length");
+	/* each thread advances SA_G walks of its block in turn: a step's one cache miss (the rank line
+	 * of the next row) is prefetched SA_G - 1 steps of the other walks before it is needed */
+	constexpr int SA_G = 16;
+	struct Walk { uint64_t i, r; uint32_t len, k; int live; };
 	std::atomic<int> bad{0};
 	par_tasks((n + 1023) / 1024, g_threads, [&](uint64_t blk) {
-		for (uint64_t i = blk * 1024; i < std::min(n, blk * 1024 + 1024); i++) {
-			uint32_t len = uv[i].length;
-			uint64_t r = i;
-			uint8_t c = rk.sym(r);
-			for (uint32_t k = 0; k < len; k++) {
-				if (c > 3) {
-					bad = 1;
+		uint64_t next = blk * 1024, end = std::min(n, blk * 1024 + 1024);
+		auto start = [&](Walk &x) {
+			x.live = next < end;
+			if (!x.live)
+				return;
+			x.i = next++;
+			x.len = uv[x.i].length;
+			x.r = x.i;
+			x.k = 0;
+			__builtin_prefetch(&rk.line[x.r >> 6]);
+		};
+		Walk w[SA_G];
+		int live = 0;
+		for (int j = 0; j < SA_G; j++) {
+			start(w[j]);
+			live += w[j].live;
+		}
+		while (live) {
+			for (int j = 0; j < SA_G; j++) {
+				Walk &x = w[j];
+				if (!x.live)
+					continue;
+				uint8_t c = rk.sym(x.r);
+				if (x.k < x.len) { /* U_i[len - 1 - k] */
+					if (c > 3) {
+						bad = 1;
+						return;
+					}
+					uint32_t off = x.len - 1 - x.k;
+					uni[st[x.i] + off] = c;
+					if ((x.r & 7) == 0) {
+						sa[x.r >> 3] = SaTaxon{(uint32_t)x.i, off};
+						filled[x.r >> 3] = 1;
+					}
+					x.r = rk.lf(x.r, c);
+					__builtin_prefetch(&rk.line[x.r >> 6]);
+					x.k++;
+					continue;
+				}
+				if (c != 4 && c != 5) { /* the separator before U_i */
+					bad = 2;
 					return;
 				}
-				uint32_t off = len - 1 - k;
-				uni[st[i] + off] = c;
-				if ((r & 7) == 0) {
-					sa[r >> 3] = SaTaxon{(uint32_t)i, off};
-					filled[r >> 3] = 1;
+				uni[st[x.i] + x.len] = (x.i == n - 1) ? 5 : 4;
+				if ((x.r & 7) == 0) {
+					uint32_t id = x.i ? (uint32_t)(x.i - 1) : (uint32_t)(n - 1);
+					sa[x.r >> 3] = SaTaxon{id, uv[id].length};
+					filled[x.r >> 3] = 1;
 				}
-				r = rk.lf(r, c);
-				c = rk.sym(r);
-			}
-			if (c != 4 && c != 5) {
-				bad = 2;
-				return;
-			}
-			uni[st[i] + len] = (i == n - 1) ? 5 : 4;
-			if ((r & 7) == 0) {
-				uint32_t id = i ? (uint32_t)(i - 1) : (uint32_t)(n - 1);
-				sa[r >> 3] = SaTaxon{id, uv[id].length};
-				filled[r >> 3] = 1;
+				start(x);
+				live -= !x.live;
 			}
 		}
 	});
