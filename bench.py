@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput of the MI355X classify path (BASELINE.json metric, config C2 at N = 1, C3 beyond).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--workload c2|c1|fixture]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--workload c2l18|c2|c2xl|c1|fixture]
                   [--mix ont|c4] [--index DIR]
 
 --gpus N without a torch.distributed launcher starts N rank processes itself (one per GPU,
@@ -14,13 +14,15 @@ results back on the host), then assign one taxon per read exactly as meta_analys
 (all_reduce over torch.distributed "nccl" when N > 1).  Reads shard across ranks (weak
 scaling: every rank classifies its own R reads); the index is replicated in each GPU's HBM.
 
-Workload C2 (the default; BASELINE configs[2], and per rank configs[3]): the C2 proxy index
-(tools/simulate.py preset c2: 495 Mbp, 286 M distinct 31-mers, so l_ek 17 / MASK_31 / 256 MB
-e-kmer tables; RefSeq itself is not available offline), built in this run by tools/proxy_build.py
-(simulate.py + this repository's desamba_index, ~60 s, cached under $TMPDIR) unless
-data/c2_index.txz is present, + R = 1M reads per rank, simulated by forked workers before the
-process touches a GPU.  Workload C1 (--workload c1): the 55.8 Mbp proxy of BASELINE configs[1]
-(data/c1_index.txz, made by the reference's own builder), usually with --reads 100000.
+Workload c2l18 (the default since round 6; BASELINE configs[2], and per rank configs[3]): a proxy of
+the RefSeq index at the reference's own index scale (tools/simulate.py preset c2l18: 1.86 Gbp,
+1.06 G distinct 31-mers, so the builder picks l_ek 18 / MASK_33 / 1 GB e-kmer tables, 1.94 G BWT
+rows, a 7.0 GB index; RefSeq itself is not available offline), built in this run by
+tools/proxy_build.py (simulate.py + this repository's desamba_index, ~2 min on the GPU box's 16
+cores, cached under $TMPDIR), + R = 1M reads per rank, simulated by forked workers before the process
+touches a GPU.  --workload c2: the smaller C2 proxy of rounds 3-5 (495 Mbp, l_ek 17, 2.3 GB);
+c2xl: 5 Gbp, BWT past 2^32 rows, 16.6 GB (an 8-minute build); c1: the 55.8 Mbp proxy of BASELINE
+configs[1] (data/c1_index.txz, made by the reference's own builder), usually with --reads 100000.
 
 The JSON line carries:
   roofline     the dominant kernel (the phase of classify part A with the largest HIP-event
@@ -432,8 +434,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reads", type=int, default=1000000, help="reads per rank")
     ap.add_argument("--mean-len", type=int, default=8000)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
-                    help="proxy index: c2 (built in the run unless data/c2_index.txz exists), c1 (data/c1_index.txz)")
+    ap.add_argument("--workload", default="c2l18", choices=sorted(WORKLOADS),
+                    help="proxy index: c2l18 (default, 7.0 GB, built in the run), c2 (2.3 GB, built in the run unless "
+                         "data/c2_index.txz exists), c2xl (16.6 GB), c1 (data/c1_index.txz)")
     ap.add_argument("--mix", default="ont", choices=["ont", "c4"], help="ONT reads, or C4's 150 bp + 20 kb 1:1 mix")
     ap.add_argument("--index", default=None, help="index directory (overrides --workload)")
     ap.add_argument("--name", default=None, help="workload name for --index")

@@ -19,6 +19,15 @@ static inline void dsb_debug_dump(FILE *f, const dsb_read_ws *w, const char *tag
 			fprintf(f, "s %u %u %u\n", x->offset, x->len, (unsigned)x->top);
 		}
 	}
+	for (int s = 0; s < 2; s++) { /* the seeding state machine's per-seed records (dsb_seed_sm: rec, klist,
+	                                 * tix, hand in the read-hash region) as the last seeding phase left
+	                                 * them, read with either strand's seed count */
+		uint32_t m = w->sd[s].l_seed_v_f;
+		const uint32_t *rec = w->hh[0];
+		for (uint32_t q = 0; q < m; q++)
+			fprintf(f, "r%d %u %08x %08x %u %u %u\n", s, q, rec[2 * q], rec[2 * q + 1], rec[2 * m + q], rec[3 * m + q],
+				rec[4 * m + q]);
+	}
 	fprintf(f, "A %s %u\n", tag, w->n_anc);
 	for (uint32_t i = 0; i < w->n_anc; i++) {
 		const dsb_anchor_t *a = w->anc + i;

@@ -1351,6 +1351,21 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 	/* ---- overflow: re-run the reads i < cn of a view whose flag is set, with 8x capacities in the
 	 * retry buffer; the view's host arrays are indexed cb + i, its device lengths / sequence offsets
 	 * are cl[i] / cso[i]: one chunk, or the deferred overflows of the whole batch (below) */
+	/* diagnostic (DSB_DEBUG_READ): a read's seeds, anchors and chains from its workspace */
+	auto debug_dump = [&](uint8_t *base, uint32_t L, uint32_t sc, const dsb_read_out_t &o, const char *tag) {
+		dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, sc));
+		std::vector<uint8_t> hbuf(lay.total);
+		HIP_OK(hipMemcpy(hbuf.data(), base, lay.total, hipMemcpyDeviceToHost));
+		dsb_read_ws w;
+		dsb_ws_init(&w, &g->h, hbuf.data(), L, dsb_default_caps(L, sc));
+		w.n_anc = o.n_anchor; w.n_hit = o.n_hit; w.fast_classify = o.fast;
+		w.overflow = o.status; w.reached_update = o.reached_update;
+		const dsb_sdir_t *sv = (const dsb_sdir_t *)(hbuf.data() + lay.state);
+		w.sd[0] = sv[0];
+		w.sd[1] = sv[1];
+		dsb_debug_dump(stderr, &w, tag);
+		return 0;
+	};
 	auto retry_view = [&](uint32_t cn, uint64_t cb, const std::vector<uint32_t> &vlen, std::vector<uint32_t> &vscale,
 			      std::vector<uint64_t> &vws_off, std::vector<dsb_read_out_t> &vro, const uint32_t *cl,
 			      const uint64_t *cso, uint8_t *wsb, uint64_t &rused, uint32_t n_over, const uint32_t *vid) -> int {
@@ -1414,6 +1429,9 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			}
 			{
 				uint64_t rbase = (uint64_t)(uintptr_t)g->wsr.p - (uint64_t)(uintptr_t)wsb + rused;
+				if (host_timing())
+					fprintf(stderr, "[dsb retry] view of %u reads: base %p, retry buffer %p (%.1f MB), rbase %#lx\n", cn,
+						(void *)wsb, g->wsr.p, g->wsr.cap / 1048576.0, (unsigned long)rbase);
 				for (uint32_t i : sel)
 					vws_off[cb + i] += rbase;
 				if (ws_fill >= 0) /* tests: the re-run reads' bytes as an earlier read's leftovers */
@@ -1446,6 +1464,10 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			hash_ms(g, 1); /* re-runs are not timed */
 			HIP_OK(copy_wait_g(g, &n_over, g->cnt.p, 4, hipMemcpyDeviceToHost, s));
 			HIP_OK(copy_wait_g(g, vro.data() + cb, g->ro.p, sizeof(dsb_read_out_t) * cn, hipMemcpyDeviceToHost, s));
+			if (const char *e = getenv("DSB_DEBUG_READ")) /* diagnostic: one re-run read's workspace */
+				for (uint32_t i : sel)
+					if (rid(i) == strtoull(e, NULL, 10))
+						debug_dump(wsb + vws_off[cb + i], vlen[cb + i], vscale[cb + i], vro[cb + i], "gpuR");
 		}
 		return 0;
 	};
@@ -1599,21 +1621,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		hs_mark(HS_RETRY);
 		if (getenv("DSB_DEBUG_READ")) { /* diagnostic: dump one read's workspace after stage A */
 			uint64_t dr = strtoull(getenv("DSB_DEBUG_READ"), NULL, 10);
-			if (dr >= cb && dr < ce) {
-				uint32_t i = (uint32_t)(dr - cb);
-				dsb_ws_layout lay = dsb_layout(len[dr], dsb_default_caps(len[dr], scale[dr]));
-				std::vector<uint8_t> hbuf(lay.total);
-				HIP_OK(hipMemcpy(hbuf.data(), wsb + ws_off[dr], lay.total, hipMemcpyDeviceToHost));
-				dsb_read_ws w;
-				dsb_ws_init(&w, &g->h, hbuf.data(), len[dr], dsb_default_caps(len[dr], scale[dr]));
-				w.n_anc = h_ro[dr].n_anchor; w.n_hit = h_ro[dr].n_hit; w.fast_classify = h_ro[dr].fast;
-				w.overflow = h_ro[dr].status; w.reached_update = h_ro[dr].reached_update;
-				(void)i;
-				const dsb_sdir_t *sv = (const dsb_sdir_t *)(hbuf.data() + lay.state);
-				w.sd[0] = sv[0];
-				w.sd[1] = sv[1];
-				dsb_debug_dump(stderr, &w, "gpuA");
-			}
+			if (dr >= cb && dr < ce)
+				debug_dump(wsb + ws_off[dr], len[dr], scale[dr], h_ro[dr], "gpuA");
 		}
 		uint64_t worst = 0;
 		for (uint32_t i = 0; i < cn; i++) {
@@ -1675,7 +1684,9 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		uint64_t need_all = 0;
 		for (uint64_t r : deferred)
 			need_all += dsb_layout(len[r], dsb_default_caps(len[r], scale[r] * DSB_CAP_RETRY)).total;
-		if (need_all + need_all / 2 > fr + g->wsr.cap && !hooks) { /* a streamed batch's other context may use it */
+		/* DSB_TEST_RELEASE_WS (test build): release it whatever the sizes */
+		if ((need_all + need_all / 2 > fr + g->wsr.cap || (DSB_TEST_HOOKS && getenv("DSB_TEST_RELEASE_WS"))) &&
+		    !hooks) { /* a streamed batch's other context may use it */
 			WS.release();
 			(void)hipMemGetInfo(&fr, &tot);
 			T.n_ws_shrink++;
@@ -1727,8 +1738,30 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 		HIP_OK(copy_wait_g(g, g->vso.p, vso.data(), 8ull * m, hipMemcpyHostToDevice, s));
 		HIP_OK(copy_wait_g(g, g->vidx.p, vidx.data(), 4ull * m, hipMemcpyHostToDevice, s));
 		uint64_t rused = 0;
-		/* offsets are relative to a base pointer only: the retry buffer's own when the chunk
-		 * workspace was released */
+		/* offsets are relative to a base pointer: the chunk workspace's, or the retry buffer's own
+		 * when the chunk workspace was released — allocated here first, for the group's first
+		 * round, so that the kernels never get a null base (with a null base and absolute
+		 * offsets, four reads of a 1M-read c2l18 batch lost a seed's anchors in the re-run) */
+		if (!WS.p) {
+			uint64_t need = 0;
+			for (uint32_t k = 0; k < m; k++)
+				need += dsb_layout(vlen[k], dsb_default_caps(vlen[k], vscale[k] * DSB_CAP_RETRY)).total;
+			need += need / 2 + 4096;
+			if (need > g->wsr.cap) {
+				g->wsr.release();
+				void *np = nullptr;
+				if (hipMalloc(&np, need) != hipSuccess) {
+					(void)hipGetLastError();
+					size_t fr2 = 0, tot2 = 0;
+					(void)hipMemGetInfo(&fr2, &tot2);
+					snprintf(err, errn, "out of HBM: %u deferred re-runs need %.1f MB of workspace, %.1f MB free on device %d",
+						 m, need / 1048576.0, fr2 / 1048576.0, g->device);
+					return -1;
+				}
+				g->wsr.p = np;
+				g->wsr.cap = need;
+			}
+		}
 		uint8_t *wsb = WS.p ? WS.as<uint8_t>() : (uint8_t *)g->wsr.p;
 		const uint32_t *vcl = g->vlen.as<uint32_t>();
 		if (retry_view(m, 0, vlen, vscale, vws, vro, vcl, g->vso.as<uint64_t>(), wsb, rused, m, vidx.data()))

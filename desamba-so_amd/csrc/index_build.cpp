@@ -13,15 +13,16 @@
  *               k-mer suffix; here positions are split over threads and the edge bits are
  *               OR-ed atomically — the same bits whatever the split.
  *   2. labels   unitig start / end flags (setLabel, idx.c:392-512): flag ORs, order-free.
- *   3. unitigs  walks from every start k-mer, in 16 index ranges as the reference's workers
- *               (get_uni_v, idx.c:723-854): unitig ids, lengths, start / end k-mers and each
- *               k-mer's preceding character (the '$' of the first range's first unitig).
+ *   3. unitigs  walks from every start k-mer (get_uni_v, idx.c:723-854): unitig ids, lengths,
+ *               start / end k-mers and each k-mer's preceding character (the '$' of the first
+ *               unitig), over successors found by one merge pass per first base (walk_unitigs_nx).
  *   4. ref lists REF_UNI records per reference segment, stable-sorted by unitig id, and the
  *               unitigs' ref_list offsets (set_ref_lists, idx.c:554-706), packed reference.
- *   5. BWT      the 30 prefix ("special") k-mers of every unitig sorted with the reference's
+ *   5. BWT      the 30 suffix ("special") k-mers of every unitig sorted with the reference's
  *               own merge schedule (ksort_stable_mt, utils.c:396-510: 15 chunks, bottom-up
- *               merges, ties to the left) — the comparator (spkmer_cmp_l, idx.c:856-880) is not
- *               a strict weak order, so only that schedule gives the reference's order — then
+ *               merges, ties to the left; spkmer_cmp_l, idx.c:856-880, orders the strings
+ *               suffix + '#' lexicographically, so the last levels' merges are cut at merge-path
+ *               points and run in parallel) — then
  *               merged with the k-mers into the BWT string and its 13-mer hash index
  *               (merge_kmer, idx.c:345-389; idx.c:933-962).
  *   6. FM index occ check points per 256 symbols, 4-bit BWT, ACGT counters (bwt.c:109-190),

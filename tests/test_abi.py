@@ -67,7 +67,8 @@ def test_load_index_fails_loudly_without_gpu(pyd, fixture_index):
 
 TEST_LIB = os.path.join(ROOT, "desamba-so_amd", "lib", "libdesamba_test.so")
 HOOK_ENV = ("DSB_TEST_SCALE0", "DSB_TEST_ROUND_ROBIN", "DSB_WAVE_PHASES", "DSB_TEST_FORCE_RERUN", "DSB_TEST_POOL_FENCED",
-            "DSB_TEST_RETRY_GROUP_MB", "DSB_TEST_WS_FILL")
+            "DSB_TEST_RETRY_GROUP_MB", "DSB_TEST_WS_FILL",
+            "DSB_TEST_RELEASE_WS")
 
 
 def _strings(path):

@@ -113,6 +113,27 @@ def test_deferred_reruns_in_groups(fixture_index, tmp_path):
     assert got[0] == want[0]
 
 
+def test_deferred_reruns_after_the_chunk_workspace_is_released(fixture_index, tmp_path):
+    """The deferred re-runs when the chunk workspace has been released for them (kernels.hip
+    batch_run: a 220-GB chunk workspace leaves too little HBM for a large group; forced here with
+    DSB_TEST_RELEASE_WS).  Round 6: the re-run kernels were then given a null workspace base with
+    absolute offsets, and four reads of a 1M-read c2l18 batch lost a replayed seed's anchors (M3's
+    NULL case, status 8, "overflows every workspace size"); the retry buffer is now allocated
+    first and is the base.  Every 2nd read re-runs (DSB_TEST_FORCE_RERUN), tiny staging makes the
+    seeding replay seeds in order (DSB_WAVE_DBG=32), workspace bytes are pre-filled
+    (DSB_TEST_WS_FILL): records byte-identical to the production library's run."""
+    fq = tmp_path / "ont_x2.fq"
+    fq.write_bytes(golden("ont.fq") * 2)
+    carry = 1 << 20
+    want, _ = run_worker(tmp_path, "prod", fixture_index, [fq], {}, lib=PROD_LIB, mode="batch", max_read_l=carry)
+    env = {"DSB_TEST_FORCE_RERUN": "2", "DSB_DEFER_RETRY": "1", "DSB_TEST_RELEASE_WS": "1", "DSB_WAVE_DBG": "32",
+           "DSB_TEST_WS_FILL": "0x5A", "DSB_HOST_TIMING": "1"}
+    got, s = run_worker(tmp_path, "released", fixture_index, [fq], env, mode="batch", max_read_l=carry)
+    assert s["calls"][0]["n_retry"] >= 2000, s["calls"][0]
+    assert "deferred re-runs" in s["stderr"]
+    assert got[0] == want[0]
+
+
 @pytest.mark.parametrize("cost", ["1", "300000"])
 def test_heavy_reads_scored_over_waves_byte_identical(fixture_index, tmp_path, cost):
     """The heavy reads' scoring (dsb_kern.h k_heavy_prep / k_heavy_spec / k_heavy_fin): every chain
