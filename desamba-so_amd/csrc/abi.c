@@ -110,6 +110,7 @@ static void copy_gpu_timing(dsb_timing_t *t, const dsb_gpu_timing *gt)
 	t->n_retry = gt->n_retry;
 	t->n_ws_shrink = gt->n_ws_shrink;
 	t->n_heavy = gt->n_heavy;
+	t->n_defer_heavy = gt->n_defer_heavy;
 	t->n_chunks = gt->n_chunks;
 	t->seed_positions = gt->seed_positions;
 	t->n_launch_dela = gt->n_launch_dela;
@@ -246,6 +247,7 @@ static void copy_timing(dsb_timing_t *t, const dsb_gpu_timing *gt)
 	t->n_retry = gt->n_retry;
 	t->n_ws_shrink = gt->n_ws_shrink;
 	t->n_heavy = gt->n_heavy;
+	t->n_defer_heavy = gt->n_defer_heavy;
 	t->n_chunks = gt->n_chunks;
 	t->seed_positions = gt->seed_positions;
 	t->n_launch_dela = gt->n_launch_dela;

@@ -40,6 +40,7 @@ typedef struct {
 	uint64_t stats[DSB_N_STATS]; /* work counters DSB_ST_*: [32*ph, 32*ph+32) phase ph, [288,320) k_classB */
 	uint64_t n_ws_shrink;    /* chunks re-partitioned smaller because their workspace did not fit in the free HBM */
 	uint64_t n_heavy;        /* scoring reads launched first as heavy (chains x length, kernels.hip k_split) */
+	uint64_t n_defer_heavy;  /* heavy reads whose scoring went to the batch's re-run group (DSB_HEAVY_DEFER) */
 } dsb_gpu_timing;
 
 /* Upload the index to `device`; -1: the DSB_DEVICES list ("all" or "0,1,..."), else the

@@ -279,6 +279,7 @@ struct dsb_gpu_dev {
 	dbuf vlen, vso, vidx, vtid; /* the deferred overflow re-runs of a batch (batch_run) */
 	dbuf hscr, hoff;         /* the heavy reads' scoring scratch and its per-read offsets (run_split) */
 	dbuf blist;              /* the scoring reads by cost class, DSB_COST_CLASSES lists of a chunk each (run_split) */
+	dbuf cbound;             /* a lower bound of the carried max_read_l before each read of a chunk (k_carry_bound) */
 	hipEvent_t evh[2][2];    /* k_hash_lds before the scoring launch, per stream (launch_phase) */
 	int evh_used[2] = {0, 0};
 	/* streamed batches (read_classify pipeline): uploads on their own stream through pinned
@@ -587,7 +588,7 @@ static void dev_free(dsb_gpu_dev *g)
 	for (void *p : g->allocs)
 		hipFree(p);
 	dbuf *bs[] = {&g->ws_off, &g->scale, &g->ws, &g->wsr, &g->order, &g->word_off, &g->ro, &g->mrl, &g->hits,
-		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2, &g->hscr, &g->hoff, &g->blist};
+		      &g->hit_off, &g->cnt, &g->stats, &g->sel, &g->wo2, &g->slist, &g->rlist, &g->cnt2, &g->hscr, &g->hoff, &g->blist, &g->cbound};
 	for (dbuf *b : bs)
 		b->release();
 	hipEventDestroy(g->ev_a);
@@ -983,15 +984,61 @@ DSB_HD uint32_t dsb_cost_class(uint64_t cost)
 	return c < DSB_COST_CLASSES - 1 ? c : DSB_COST_CLASSES - 1;
 }
 
-/* cnt: [0] slow, [1] heavy (spec), [2 + c] class c; class c's reads at classes + c * n */
+/* Heavy reads deferred to the end of the batch (DSB_HEAVY_DEFER, cost >= DSB_DEFER_COST).  A scoring
+ * launch lasts at least as long as its costliest read's wave: on the c2xl proxy the launch's wave clocks
+ * summed to the small proxy's, but every launch waited ~140 ms for its heaviest read (one per chunk
+ * and list, ten per step).  Such a read leaves the chunk's scoring with status DSB_STATUS_DEFER_HEAVY and
+ * is classified again with the batch's deferred overflow re-runs, so the tails of all chunks overlap in
+ * one launch.  A read may go only when its own result cannot move the carried max_read_l
+ * (src/cly.c:2953): its length is at most a lower bound of the carry before it — the batch's carry-in
+ * and the prefix maximum of the lengths of the chunk's earlier reads known to reach the update (fast
+ * reads with hits after resolve_f: delete_small_score_rst returns early only without hits), computed by
+ * k_carry_bound. */
+#define DSB_STATUS_DEFER_HEAVY 64u
+#define DSB_CB_WG 1024
+__global__ __launch_bounds__(DSB_CB_WG) void k_carry_bound(const uint32_t *__restrict__ len, const uint64_t *__restrict__ ws_off,
+							   const uint32_t *__restrict__ scale, const uint8_t *__restrict__ ws, uint32_t n,
+							   uint32_t *__restrict__ bound)
+{
+	__shared__ uint32_t part[DSB_CB_WG];
+	uint32_t tid = threadIdx.x, per = (n + DSB_CB_WG - 1) / DSB_CB_WG;
+	uint32_t lo = DSB_MIN(n, tid * per), hi = DSB_MIN(n, lo + per);
+	auto val = [&](uint32_t i) -> uint32_t { /* read i (input order) reaches the update with its length */
+		uint32_t L = len[i];
+		dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, scale[i]));
+		const dsb_rstate_t *sp = (const dsb_rstate_t *)(ws + ws_off[i] + lay.state);
+		return (!sp->f.done && !sp->overflow && !sp->f.run_slow && sp->n_hit) ? L : 0u;
+	};
+	uint32_t m = 0;
+	for (uint32_t i = lo; i < hi; i++)
+		m = DSB_MAX(m, val(i));
+	part[tid] = m;
+	__syncthreads();
+	for (uint32_t off = 1; off < DSB_CB_WG; off <<= 1) { /* inclusive prefix max over the threads' ranges */
+		uint32_t v = tid >= off ? part[tid - off] : 0u;
+		__syncthreads();
+		part[tid] = DSB_MAX(part[tid], v);
+		__syncthreads();
+	}
+	uint32_t run = tid ? part[tid - 1] : 0u;
+	for (uint32_t i = lo; i < hi; i++) {
+		bound[i] = run;
+		run = DSB_MAX(run, val(i));
+	}
+}
+
+/* cnt: [0] slow, [1] heavy (spec), [2 + c] class c, [2 + DSB_COST_CLASSES] deferred (DSB_HEAVY_DEFER);
+ * class c's reads at classes + c * n */
 __global__ __launch_bounds__(64) void k_split(const uint32_t *__restrict__ len, const uint64_t *__restrict__ ws_off,
 					      const uint32_t *__restrict__ scale, const uint8_t *__restrict__ ws,
 					      const uint32_t *__restrict__ order, uint32_t n, uint32_t *__restrict__ slow_list,
 					      uint32_t *__restrict__ heavy_list, uint32_t *__restrict__ classes,
-					      uint32_t *__restrict__ cnt, uint32_t heavy)
+					      uint32_t *__restrict__ cnt, uint32_t heavy, uint32_t defer_cost,
+					      const uint32_t *__restrict__ bound, uint32_t carry_in, dsb_read_out_t *__restrict__ ro,
+					      uint32_t *__restrict__ n_overflow)
 {
 	uint32_t t = blockIdx.x * 64 + threadIdx.x, lane = threadIdx.x;
-	int act = t < n, slow = 0, hv = 0;
+	int act = t < n, slow = 0, hv = 0, df = 0;
 	uint32_t r = 0, cls = 0;
 	if (act) {
 		r = order[t];
@@ -1003,18 +1050,25 @@ __global__ __launch_bounds__(64) void k_split(const uint32_t *__restrict__ len, 
 		/* the heavy reads' waves share the read hash k_hash_lds prebuilt: a read whose hash each
 		 * wave would build itself (dsb_hash_lds_read false) stays in the one-wave scoring */
 		hv = !slow && sp->n_hit && cost >= heavy && dsb_hash_lds_read(L);
+		df = !slow && !hv && sp->n_hit && cost >= defer_cost && L <= DSB_MAX(carry_in, bound[r]);
 		cls = dsb_cost_class(cost);
+		if (df) {
+			dsb_read_out_t o = {0, 0, 0, DSB_STATUS_DEFER_HEAVY, 0, 0, 0};
+			ro[r] = o;
+			atomicAdd(n_overflow, 1u);
+		}
 	}
 	uint64_t lt = lane == 0 ? 0 : (~0ull >> (64 - lane));
 	/* slow and heavy lists, then each class present in the wave: one atomic per list per wave */
-	int key = !act ? -1 : slow ? DSB_COST_CLASSES : hv ? DSB_COST_CLASSES + 1 : (int)cls;
+	int key = !act ? -1 : slow ? DSB_COST_CLASSES : hv ? DSB_COST_CLASSES + 1 : df ? DSB_COST_CLASSES + 2 : (int)cls;
 	for (;;) {
 		uint64_t live = __ballot(key >= 0);
 		if (!live)
 			break;
 		int k0 = __shfl(key, (int)__builtin_ctzll(live));
 		uint64_t m = __ballot(key == k0);
-		uint32_t *ctr = k0 == DSB_COST_CLASSES ? cnt : k0 == DSB_COST_CLASSES + 1 ? cnt + 1 : cnt + 2 + k0;
+		uint32_t *ctr = k0 == DSB_COST_CLASSES ? cnt : k0 == DSB_COST_CLASSES + 1 ? cnt + 1 :
+				k0 == DSB_COST_CLASSES + 2 ? cnt + 2 + DSB_COST_CLASSES : cnt + 2 + k0;
 		uint32_t base = 0;
 		if (lane == (uint32_t)__builtin_ctzll(m))
 			base = atomicAdd(ctr, (uint32_t)__builtin_popcountll(m));
@@ -1025,7 +1079,7 @@ __global__ __launch_bounds__(64) void k_split(const uint32_t *__restrict__ len, 
 				slow_list[at] = r;
 			else if (k0 == DSB_COST_CLASSES + 1)
 				heavy_list[at] = r;
-			else
+			else if (k0 < DSB_COST_CLASSES)
 				classes[(uint64_t)k0 * n + at] = r;
 			key = -1;
 		}
@@ -1109,32 +1163,60 @@ static int heavy_spec(void)
 	return v;
 }
 
+/* DSB_HEAVY_DEFER=1: heavy reads' scoring deferred to the batch's re-run group (k_split), reads of cost
+ * >= DSB_DEFER_COST (chains x length) */
+#ifndef DSB_DEFER_COST
+#define DSB_DEFER_COST (1u << 22)
+#endif
+static uint32_t defer_cost(void)
+{
+	static int64_t v = -1;
+	if (v < 0) {
+		const char *e = getenv("DSB_HEAVY_DEFER");
+		const char *c = getenv("DSB_DEFER_COST");
+		v = (e && atoi(e)) ? (c ? strtoll(c, NULL, 10) : DSB_DEFER_COST) : UINT32_MAX;
+	}
+	return (uint32_t)v;
+}
+
+static int defer_retries(void);
+
+/* carry_in: the carried max_read_l before the chunk when known (else 0: a lower bound) */
 static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb, uint32_t cn, const uint32_t *hlen,
-		     const uint32_t *hscale, dsb_gpu_timing &T, char *err, size_t errn)
+		     const uint32_t *hscale, uint32_t carry_in, dsb_gpu_timing &T, char *err, size_t errn)
 {
 	hipStream_t s = g->stream;
 	/* slist: the slow reads, then (at cn) the heavy scoring reads (DSB_HEAVY_SPEC); blist: the
 	 * other scoring reads by cost class; rlist: those, costliest class first */
 	const int want_spec = stats == 0 && heavy_spec();
+	/* heavy reads deferred to the batch's re-run group (not in stats runs: those count every read's
+	 * work in its chunk's phases; not without deferral) */
+	const uint32_t dcost = (stats == 0 && defer_retries()) ? defer_cost() : UINT32_MAX;
 	if (g->slist.ensure(8ull * cn + 8, err, errn) || g->rlist.ensure(4ull * cn + 4, err, errn) ||
-	    g->blist.ensure(4ull * DSB_COST_CLASSES * cn + 4, err, errn) || g->cnt2.ensure(4 * (2 + DSB_COST_CLASSES), err, errn))
+	    g->blist.ensure(4ull * DSB_COST_CLASSES * cn + 4, err, errn) || g->cnt2.ensure(4 * (3 + DSB_COST_CLASSES), err, errn) ||
+	    g->cbound.ensure(4ull * cn + 4, err, errn))
 		return -1;
-	HIP_OK(hipMemsetAsync(g->cnt2.p, 0, 4 * (2 + DSB_COST_CLASSES), s));
+	HIP_OK(hipMemsetAsync(g->cnt2.p, 0, 4 * (3 + DSB_COST_CLASSES), s));
+	if (dcost != UINT32_MAX)
+		k_carry_bound<<<1, DSB_CB_WG, 0, s>>>(cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, cn,
+						       g->cbound.as<uint32_t>());
 	uint32_t *hl = g->slist.as<uint32_t>() + cn;
 	k_split<<<(cn + 63) / 64, 64, 0, s>>>(cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb,
 					       g->order.as<uint32_t>(), cn, g->slist.as<uint32_t>(), hl, g->blist.as<uint32_t>(),
-					       g->cnt2.as<uint32_t>(), want_spec ? heavy_cost() : UINT32_MAX);
+					       g->cnt2.as<uint32_t>(), want_spec ? heavy_cost() : UINT32_MAX, dcost,
+					       g->cbound.as<uint32_t>(), carry_in, g->ro.as<dsb_read_out_t>(), g->cnt.as<uint32_t>());
 	HIP_OK(hipGetLastError());
-	uint32_t cc[2 + DSB_COST_CLASSES];
+	uint32_t cc[3 + DSB_COST_CLASSES];
 	HIP_OK(copy_wait_g(g, cc, g->cnt2.p, sizeof(cc), hipMemcpyDeviceToHost, s));
 	uint32_t nr = 0;
 	for (int k = 0; k < DSB_COST_CLASSES; k++)
 		nr += cc[2 + k];
-	uint32_t nh = cc[1];
-	if (cc[0] + nh + nr != cn) {
-		snprintf(err, errn, "split: %u + %u + %u reads for a chunk of %u", cc[0], nh, nr, cn);
+	uint32_t nh = cc[1], nd = cc[2 + DSB_COST_CLASSES];
+	if (cc[0] + nh + nr + nd != cn) {
+		snprintf(err, errn, "split: %u + %u + %u + %u reads for a chunk of %u", cc[0], nh, nr, nd, cn);
 		return -1;
 	}
+	T.n_defer_heavy += nd;
 	if (cc[0] == 0 || nh + nr == 0)
 		return 0;
 	/* the rest of the reads' list, costliest class first */
@@ -1567,7 +1649,8 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 			}
 			HIP_OK(hipGetLastError());
 			if (ph == DSB_PH_RESOLVE_F && split_slow()) {
-				int r = run_split(g, stats_on, cl, wsb, cn, len.data() + cb, scale.data() + cb, T, err, errn);
+				int r = run_split(g, stats_on, cl, wsb, cn, len.data() + cb, scale.data() + cb,
+						  hooks ? 0u : (uint32_t)DSB_MAX(carry, 0), T, err, errn);
 				if (r < 0)
 					return -1;
 				if (r == 1) /* the rest of part A ran split */

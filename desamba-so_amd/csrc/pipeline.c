@@ -195,6 +195,7 @@ static void acc_timing(dsb_gpu_timing *a, const dsb_gpu_timing *b)
 	a->n_retry += b->n_retry;
 	a->n_ws_shrink += b->n_ws_shrink;
 	a->n_heavy += b->n_heavy;
+	a->n_defer_heavy += b->n_defer_heavy;
 	a->n_chunks += b->n_chunks;
 	a->seed_positions += b->seed_positions;
 	a->n_launch_dela += b->n_launch_dela;

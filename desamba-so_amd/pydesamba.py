@@ -34,7 +34,7 @@ class Timing(C.Structure):
                 ("ms_parse", C.c_double), ("ms_gather", C.c_double), ("ms_format", C.c_double),
                 ("ms_wait_gpu", C.c_double), ("n_batches", C.c_uint64), ("n_devices", C.c_uint64),
                 ("n_view_records", C.c_uint64), ("n_copied_records", C.c_uint64),
-                ("n_ws_shrink", C.c_uint64), ("n_heavy", C.c_uint64)]
+                ("n_ws_shrink", C.c_uint64), ("n_heavy", C.c_uint64), ("n_defer_heavy", C.c_uint64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in ("stats", "ms_phase")}

@@ -27,6 +27,7 @@ typedef struct {
 	uint64_t n_batches, n_devices, n_view_records, n_copied_records;
 	uint64_t n_ws_shrink;  /* chunks re-partitioned smaller: their workspace did not fit in the free HBM */
 	uint64_t n_heavy;      /* scoring reads launched first (many chains of a long read) */
+	uint64_t n_defer_heavy; /* heavy reads classified with the batch's deferred re-runs (DSB_HEAVY_DEFER) */
 } dsb_timing_t;
 
 /* Classify FASTQ/FASTA text.  format: 1 SAM, 2 SAM_FULL, 3 DES, 4 DES_FULL.
