@@ -529,29 +529,72 @@ template <class IX> void walk_unitigs_nx(Kmers &km, uint64_t n_uni, Unitigs &u)
 			first_start = i;
 			break;
 		}
+	/* each thread advances UW walks of its slice in turn, the next k-mer's successor index and
+	 * flags prefetched UW - 1 steps of the other walks before they are needed (one dependent cache
+	 * miss per step otherwise: 113 of the c2xl build's 322 s); the slice's unitigs keep the order of
+	 * their start k-mers */
+	constexpr int UW = 16;
 	std::vector<Unitigs> part(n_sl);
 	par_tasks(n_sl, g_threads, [&](uint64_t s) {
 		uint64_t lo = s * SLICE, hi = std::min(n, lo + SLICE);
 		Unitigs &p = part[s];
-		for (uint64_t i = lo; i < hi; i++) {
-			if (!(ld16(info + i) & F_START))
-				continue;
-			or16(info + i, (uint16_t)((i == first_start ? 5u : 4u) << 10));
-			uint64_t loc = i;
-			uint32_t L = K;
-			uint16_t x = ld16(info + loc);
-			while (!(x & F_END)) {
-				loc = nx[loc];
-				x = ld16(info + loc);
-				unsigned in = (x >> 4) & 15u;
-				if (popc4(in) != 1)
-					die("unitig walk: a successor without exactly one in edge");
-				or16(info + loc, (uint16_t)((unsigned)__builtin_ctz(in) << 10));
-				L++;
+		uint64_t ns = 0;
+		for (uint64_t i = lo; i < hi; i++)
+			ns += (ld16(info + i) & F_START) != 0;
+		p.len.resize(ns);
+		p.start.resize(ns);
+		p.end.resize(ns);
+		/* a walk's current k-mer is `loc`; `pend`: its preceding character is still to be OR-ed
+		 * (done on the walk's next turn, when its flags line has arrived) */
+		struct Walk { uint64_t i, loc, slot; uint32_t L; int live, pend; };
+		uint64_t next = lo, slot = 0;
+		auto start = [&](Walk &x) {
+			while (next < hi && !(ld16(info + next) & F_START))
+				next++;
+			x.live = next < hi;
+			if (!x.live)
+				return;
+			x.i = x.loc = next++;
+			x.slot = slot++;
+			x.L = K;
+			x.pend = 0;
+			or16(info + x.i, (uint16_t)((x.i == first_start ? 5u : 4u) << 10));
+			__builtin_prefetch(&nx[x.loc]);
+		};
+		Walk w[UW];
+		int live = 0;
+		for (int j = 0; j < UW; j++) {
+			start(w[j]);
+			live += w[j].live;
+		}
+		while (live) {
+			for (int j = 0; j < UW; j++) {
+				Walk &x = w[j];
+				if (!x.live)
+					continue;
+				uint16_t f = ld16(info + x.loc);
+				if (x.pend) {
+					unsigned in = (f >> 4) & 15u;
+					if (popc4(in) != 1)
+						die("unitig walk: a successor without exactly one in edge");
+					or16(info + x.loc, (uint16_t)((unsigned)__builtin_ctz(in) << 10));
+					x.pend = 0;
+				}
+				if (!(f & F_END)) { /* one step: the successor's flags and successor index prefetched */
+					uint64_t nl = nx[x.loc];
+					__builtin_prefetch(info + nl);
+					__builtin_prefetch(&nx[nl]);
+					x.loc = nl;
+					x.L++;
+					x.pend = 1;
+					continue;
+				}
+				p.end[x.slot] = v[x.loc];
+				p.len[x.slot] = x.L;
+				p.start[x.slot] = v[x.i];
+				start(x);
+				live -= !x.live;
 			}
-			p.end.push_back(v[loc]);
-			p.len.push_back(L);
-			p.start.push_back(v[i]);
 		}
 	});
 	for (auto &p : part) {
