@@ -585,6 +585,16 @@ __device__ __forceinline__ void dsb_hpool_release(const dsb_dindex_t *ix, uint32
 #define DSB_HSET_LDS 1
 #endif
 
+/* resolve_tree fused into the seeding kernels (wave_phase_read; the host skips the resolve launches,
+ * kernels.hip resolve_fused).  Parity-green, but slower on c2l18 (A/B, 3 steps: 517.9k fused vs
+ * 523.8k separate): the fused fast-seeding kernel spills 432 B per lane instead of 192, and fast
+ * seeding grew by more than the resolve launch it absorbed (642 + 48 -> 715 ms per step).  Off. */
+#ifndef DSB_FUSE_RESOLVE
+#define DSB_FUSE_RESOLVE 0
+#endif
+/* the seeding kernels' LDS buffer: the sp_set first level, then the fused resolve's sort arrays */
+#define DSB_SEED_LDS_U64 DSB_MAX((DSB_HSET_LDS ? DSB_HSET_L1 * 64u : 1u), (12u * DSB_MAX(DSB_SORT_LDS, DSB_SORT_LDS_SLOW) + 7u) / 8u)
+
 /* Lanes per read of the seeding phases (FAST0/1, SLOW0/1): 64 = a wave per read; 32 = two reads
  * per wave, each on a half-wave group running the state machine of dsb_seed_sm on its own (a
  * read's wave time is set by its longest seed, so the other lanes mostly wait: tools/seed_prof). */
@@ -672,9 +682,10 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 			uint64_t hs_tag = dsb_hset_tag(&w);
 			uint32_t last_gen;
 #endif
-			/* LDS: per group, 2 x G ints (dsb_seed_sm's owner / max arrays) */
-			/* the sp_set's first level (dsb_set_insert): DSB_HSET_L1 u64 per lane, 16 KB per wave */
-			__shared__ uint64_t hs_l1[DSB_HSET_LDS ? DSB_HSET_L1 * 64 : 1];
+			/* LDS: per group, 2 x G ints (dsb_seed_sm's owner / max arrays); the sp_set's first level
+			 * (dsb_set_insert: DSB_HSET_L1 u64 per lane, 16 KB per wave), reused after the seeding by the
+			 * fused resolve's sort arrays */
+			__shared__ uint64_t hs_l1[DSB_SEED_LDS_U64];
 			if (ph == DSB_PH_FAST0 || ph == DSB_PH_FAST1) {
 				__shared__ int32_t sm_lds[2 * 64];
 				last_gen = dsb_fast_classify_sm<G>(&w, &w.sd[ph - DSB_PH_FAST0], hset, hs_tag, sm_lds, DSB_HSET_LDS ? hs_l1 : nullptr);
@@ -686,6 +697,22 @@ __device__ __forceinline__ void wave_phase_read(const dsb_dindex_t *__restrict__
 #if !DSB_HSET_POOL
 			(void)last_gen;
 #endif
+			/* the read's resolve right after its seeding (DSB_FUSE_RESOLVE): resolve_tree of the fast
+			 * reads after their last fast phase, of the slow reads after each slow phase — the same
+			 * per-read steps in the same order as separate launches, but a read with a long resolve
+			 * runs it beside the other reads' seeding instead of as the tail of a launch of its own */
+			if (DSB_FUSE_RESOLVE && STATS == 0 && G == 64) {
+				const int rph = ((ph == DSB_PH_FAST0 && !f.both) || ph == DSB_PH_FAST1) ? DSB_PH_RESOLVE_F
+						: ph == DSB_PH_SLOW0 ? DSB_PH_RESOLVE_S0 : ph == DSB_PH_SLOW1 ? DSB_PH_RESOLVE_S1 : -1;
+				if (rph >= 0) {
+					const uint32_t NS = rph == DSB_PH_RESOLVE_F ? DSB_SORT_LDS : DSB_SORT_LDS_SLOW;
+					dsb_wsync();
+					w.lds_key = hs_l1;
+					w.lds_id = (uint32_t *)(hs_l1 + NS);
+					w.lds_n = NS;
+					dsb_phase<true>(&w, &f, rph);
+				}
+			}
 		} else if (ph == DSB_PH_RESOLVE_F || ph == DSB_PH_RESOLVE_S0 || ph == DSB_PH_RESOLVE_S1) {
 			constexpr uint32_t NS = (PH == DSB_PH_RESOLVE_S0 || PH == DSB_PH_RESOLVE_S1) ? DSB_SORT_LDS_SLOW : DSB_SORT_LDS;
 			__shared__ uint64_t sort_key[NS];

@@ -834,11 +834,28 @@ static float hash_ms(dsb_gpu_dev *g, int clear = 0)
 }
 
 /* one phase of part A over the reads order[0..m) */
+/* the resolve phase ph ran inside the seeding kernels before it (dsb_kern.h DSB_FUSE_RESOLVE; not in
+ * the stats runs, whose counters stay per phase, nor with lane-per-read seeding kernels) */
+static int resolve_fused(int ph, int stats)
+{
+	if (!DSB_FUSE_RESOLVE || stats || DSB_SM_G != 64)
+		return 0;
+	uint32_t wp = wave_phases();
+	switch (ph) {
+	case DSB_PH_RESOLVE_F: return ((wp >> DSB_PH_FAST0) & 1) && ((wp >> DSB_PH_FAST1) & 1);
+	case DSB_PH_RESOLVE_S0: return (wp >> DSB_PH_SLOW0) & 1;
+	case DSB_PH_RESOLVE_S1: return (wp >> DSB_PH_SLOW1) & 1;
+	default: return 0;
+	}
+}
+
 static void launch_phase(dsb_gpu_dev *g, int ph, int stats, const uint32_t *cl, uint8_t *wsb, const uint32_t *order,
 			 uint32_t m, hipStream_t s = 0)
 {
 	if (!s)
 		s = g->stream;
+	if (resolve_fused(ph, stats))
+		return;
 	int wave = (int)((wave_phases() >> ph) & 1);
 	dsb_phase_fn fn = phase_kernel_at(ph, wave, stats);
 	if (!fn) { /* a lane-per-read phase variant that is not compiled in (build with DSB_LANE_PHASES=1) */
