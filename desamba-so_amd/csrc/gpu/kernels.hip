@@ -355,6 +355,7 @@ static int dev_init(dsb_index *ix, int device, const dsb_gpu_dev *share, dsb_gpu
 	g->device = device;
 	pthread_mutex_init(&g->mu, NULL);
 	pthread_mutex_init(&g->umu, NULL);
+	/* default priority: at the highest one the slow reads' chain was no faster (r06_c2l18/ab_stream_prio.txt) */
 	HIP_OK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
 	HIP_OK(hipStreamCreateWithFlags(&g->cstream, hipStreamNonBlocking));
 	for (int k = 0; k < 2; k++)
