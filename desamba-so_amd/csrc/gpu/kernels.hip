@@ -1328,6 +1328,111 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 	return 1;
 }
 
+/* The scoring of an overflow re-run (retry_view) with its heavy reads (cost >= DSB_HEAVY_COST,
+ * k_split's rule) over DSB_HEAVY_W waves each (k_heavy_*) beside the one-wave scoring of the rest
+ * (default; DSB_RETRY_SPEC=0: one wave per read).  A re-run group is a few hundred of the batch's
+ * costliest reads and its scoring launch lasts as long as the costliest one (43 of the 82 ms of a
+ * c2l18 step's re-run tail).  Every phase before the scoring has run for every re-run read, slow
+ * ones included, so the list takes any read with chains to score.  c2l18: 541.6k vs 538.6k reads/s
+ * (profiles/r06_c2l18/ab_retry_spec.txt). */
+#ifndef DSB_RETRY_SPEC_DEFAULT
+#define DSB_RETRY_SPEC_DEFAULT 1
+#endif
+static int retry_spec(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("DSB_RETRY_SPEC");
+		v = e ? (atoi(e) != 0) : DSB_RETRY_SPEC_DEFAULT;
+	}
+	return v && DSB_HASH_LDS;
+}
+
+/* cnt: [0] heavy reads (heavy_list), [1] the others (rest_list) */
+__global__ __launch_bounds__(64) void k_retry_split(const uint32_t *__restrict__ len, const uint64_t *__restrict__ ws_off,
+						    const uint32_t *__restrict__ scale, const uint8_t *__restrict__ ws,
+						    const uint32_t *__restrict__ sel, uint32_t n, uint32_t heavy,
+						    uint32_t *__restrict__ heavy_list, uint32_t *__restrict__ rest_list,
+						    uint32_t *__restrict__ cnt)
+{
+	uint32_t t = blockIdx.x * 64 + threadIdx.x;
+	if (t >= n)
+		return;
+	uint32_t r = sel[t], L = len[r];
+	dsb_ws_layout lay = dsb_layout(L, dsb_default_caps(L, scale[r]));
+	const dsb_rstate_t *sp = (const dsb_rstate_t *)(ws + ws_off[r] + lay.state);
+	uint64_t cost = (!sp->f.done && !sp->overflow) ? (uint64_t)DSB_MIN(sp->n_hit, 400u) * L : 0;
+	if (sp->n_hit && cost >= heavy && dsb_hash_lds_read(L))
+		heavy_list[atomicAdd(cnt, 1u)] = r;
+	else
+		rest_list[atomicAdd(cnt + 1, 1u)] = r;
+}
+
+/* the scoring phase of a re-run of the m reads sel[] (device list; hlen / hscale: the view's host
+ * lengths and capacity scales by read) -> the number of reads scored over several waves, or -1 */
+static int retry_score(dsb_gpu_dev *g, const uint32_t *cl, uint8_t *wsb, const uint32_t *sel, uint32_t m,
+		       const uint32_t *hlen, const uint32_t *hscale, char *err, size_t errn)
+{
+	hipStream_t s = g->stream;
+	if (g->slist.ensure(4ull * m + 4, err, errn) || g->rlist.ensure(4ull * m + 4, err, errn) ||
+	    g->cnt2.ensure(4 * (3 + DSB_COST_CLASSES), err, errn))
+		return -1;
+	HIP_OK(hipMemsetAsync(g->cnt2.p, 0, 8, s));
+	k_retry_split<<<(m + 63) / 64, 64, 0, s>>>(cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, sel, m,
+						   heavy_cost(), g->slist.as<uint32_t>(), g->rlist.as<uint32_t>(),
+						   g->cnt2.as<uint32_t>());
+	HIP_OK(hipGetLastError());
+	uint32_t cc[2];
+	HIP_OK(copy_wait_g(g, cc, g->cnt2.p, sizeof(cc), hipMemcpyDeviceToHost, s));
+	const uint32_t nh = cc[0], nr = cc[1];
+	if (nh + nr != m) {
+		snprintf(err, errn, "re-run split: %u + %u reads of %u", nh, nr, m);
+		return -1;
+	}
+	if (!nh) {
+		launch_phase(g, DSB_PH_DELA, 0, cl, wsb, sel, m);
+		return 0;
+	}
+	static dsb_heavy_prep_fn k_prep;
+	static dsb_heavy_spec_fn k_spec;
+	static dsb_heavy_fin_fn k_fin;
+	if (!k_prep)
+		dsb_heavy_kernels(&k_prep, &k_spec, &k_fin);
+	const uint32_t *hl = g->slist.as<uint32_t>();
+	std::vector<uint32_t> hv(nh);
+	HIP_OK(copy_wait_g(g, hv.data(), hl, 4ull * nh, hipMemcpyDeviceToHost, s));
+	std::vector<uint64_t> ho(nh);
+	uint64_t tot = 0;
+	for (uint32_t k = 0; k < nh; k++) {
+		ho[k] = tot;
+		tot += dsb_heavy_bytes(hlen[hv[k]], hscale[hv[k]]);
+	}
+	if (g->hscr.ensure(tot + 256, err, errn) || g->hoff.ensure(8ull * nh + 8, err, errn))
+		return -1;
+	HIP_OK(copy_wait_g(g, g->hoff.p, ho.data(), 8ull * nh, hipMemcpyHostToDevice, s));
+	if (!g->stream3)
+		HIP_OK(hipStreamCreateWithPriority(&g->stream3, hipStreamNonBlocking, g->prio_hi));
+	const uint32_t dbg = wave_dbg();
+	hipEventRecord(g->ev_fork, s);
+	HIP_OK(hipStreamWaitEvent(g->stream3, g->ev_fork, 0));
+	hipLaunchKernelGGL(k_hash_lds<0>, dim3(2 * nh), dim3(DSB_HL_WG), 0, g->stream3, g->d, cl, g->ws_off.as<uint64_t>(),
+			   g->scale.as<uint32_t>(), wsb, hl, nh, g->stats.as<unsigned long long>());
+	hipLaunchKernelGGL(k_prep, dim3(nh), dim3(64), 0, g->stream3, g->d, cl, g->ws_off.as<uint64_t>(),
+			   g->scale.as<uint32_t>(), wsb, hl, nh, dbg);
+	hipLaunchKernelGGL(k_spec, dim3(nh * DSB_HEAVY_W), dim3(64), 0, g->stream3, g->d, cl, g->ws_off.as<uint64_t>(),
+			   g->scale.as<uint32_t>(), wsb, hl, nh, g->hscr.as<uint8_t>(), g->hoff.as<uint64_t>(), dbg);
+	hipLaunchKernelGGL(k_fin, dim3(nh), dim3(64), 0, g->stream3, g->d, cl, g->ws_off.as<uint64_t>(),
+			   g->scale.as<uint32_t>(), wsb, hl, nh, g->hscr.as<uint8_t>(), g->hoff.as<uint64_t>(),
+			   g->ro.as<dsb_read_out_t>(), g->cnt.as<uint32_t>(), dbg);
+	hipEventRecord(g->ev_h1, g->stream3);
+	HIP_OK(hipGetLastError());
+	if (nr)
+		launch_phase(g, DSB_PH_DELA, 0, cl, wsb, g->rlist.as<uint32_t>(), nr);
+	HIP_OK(hipStreamWaitEvent(s, g->ev_h1, 0));
+	HIP_OK(hipGetLastError());
+	return (int)nh;
+}
+
 /* DSB_HOST_TIMING=1 (diagnostic): per batch_run, the host wall time of each section of the chunk
  * loop on stderr (the GPU idles in the sections that end in a synchronisation) */
 enum { HS_SIZE, HS_SETUP, HS_PARTA, HS_SYNC_A, HS_RETRY, HS_CARRY_B, HS_D2H, HS_N };
@@ -1556,8 +1661,16 @@ static int batch_run(dsb_gpu_dev *g, dsb_index *ix, dsb_gpu_batch *b, int *max_r
 				k_seed<<<(uint32_t)((tw2 * 64 + 255) / 256), 256, 0, s>>>(g->d, cl, g->ws_off.as<uint64_t>(), wsb,
 											      g->wo2.as<uint64_t>(), g->sel.as<uint32_t>(), m, tw2, nullptr);
 			HIP_OK(hipMemsetAsync(g->cnt.p, 0, 64, s));
-			for (int ph = 0; ph < DSB_PH_N; ph++)
+			const int rspec = retry_spec();
+			for (int ph = 0; ph < (rspec ? DSB_PH_DELA : DSB_PH_N); ph++)
 				launch_phase(g, ph, false, cl, wsb, g->sel.as<uint32_t>(), m);
+			if (rspec) {
+				int nh = retry_score(g, cl, wsb, g->sel.as<uint32_t>(), m, vlen.data() + cb, vscale.data() + cb, err, errn);
+				if (nh < 0)
+					return -1;
+				if (host_timing())
+					fprintf(stderr, "[dsb retry] %d of %u re-run reads scored over %d waves each\n", nh, m, DSB_HEAVY_W);
+			}
 			HIP_OK(hipGetLastError());
 			/* the re-run went to the non-blocking stream: drain it before the (null-stream) copies */
 			HIP_OK(hipStreamSynchronize(s));
