@@ -1328,8 +1328,8 @@ static int run_split(dsb_gpu_dev *g, int stats, const uint32_t *cl, uint8_t *wsb
 	return 1;
 }
 
-/* The scoring of an overflow re-run (retry_view) with its heavy reads (cost >= DSB_HEAVY_COST,
- * k_split's rule) over DSB_HEAVY_W waves each (k_heavy_*) beside the one-wave scoring of the rest
+/* The scoring of an overflow re-run (retry_view) with its heavy reads (cost >= DSB_RETRY_HEAVY_COST,
+ * k_split's rule otherwise) over DSB_HEAVY_W waves each (k_heavy_*) beside the one-wave scoring of the rest
  * (default; DSB_RETRY_SPEC=0: one wave per read).  A re-run group is a few hundred of the batch's
  * costliest reads and its scoring launch lasts as long as the costliest one (43 of the 82 ms of a
  * c2l18 step's re-run tail).  Every phase before the scoring has run for every re-run read, slow
@@ -1346,6 +1346,23 @@ static int retry_spec(void)
 		v = e ? (atoi(e) != 0) : DSB_RETRY_SPEC_DEFAULT;
 	}
 	return v && DSB_HASH_LDS;
+}
+
+/* the re-run's heavy-read threshold (chains x length, DSB_RETRY_HEAVY_COST): 1 = every re-run read with
+ * a chain to score.  The re-run's reads are few and costly, and its one-wave tail was a read below
+ * the chunk's threshold: c2l18 550.7k reads/s at 1, 550.4k at 2^16, 541.7k at DSB_HEAVY_COST's 2^20
+ * (profiles/r06_c2l18/ab_retry_cost.txt) */
+#ifndef DSB_RETRY_HEAVY_COST
+#define DSB_RETRY_HEAVY_COST 1
+#endif
+static uint32_t retry_heavy_cost(void)
+{
+	static int64_t v = -1;
+	if (v < 0) {
+		const char *e = getenv("DSB_RETRY_HEAVY_COST");
+		v = e ? strtoll(e, NULL, 10) : (int64_t)DSB_RETRY_HEAVY_COST;
+	}
+	return (uint32_t)v;
 }
 
 /* cnt: [0] heavy reads (heavy_list), [1] the others (rest_list) */
@@ -1379,7 +1396,7 @@ static int retry_score(dsb_gpu_dev *g, const uint32_t *cl, uint8_t *wsb, const u
 		return -1;
 	HIP_OK(hipMemsetAsync(g->cnt2.p, 0, 8, s));
 	k_retry_split<<<(m + 63) / 64, 64, 0, s>>>(cl, g->ws_off.as<uint64_t>(), g->scale.as<uint32_t>(), wsb, sel, m,
-						   heavy_cost(), g->slist.as<uint32_t>(), g->rlist.as<uint32_t>(),
+						   retry_heavy_cost(), g->slist.as<uint32_t>(), g->rlist.as<uint32_t>(),
 						   g->cnt2.as<uint32_t>());
 	HIP_OK(hipGetLastError());
 	uint32_t cc[2];

@@ -159,15 +159,15 @@ def test_rerun_heavy_reads_scored_over_waves_byte_identical(fixture_index, tmp_p
     """DSB_RETRY_SPEC=1 (kernels.hip retry_score): an overflow re-run scores its heavy reads over
     DSB_HEAVY_W waves each beside the one-wave scoring of the rest; unlike the chunk's split, the
     re-run's list also takes reads that went through slow seeding.  Every 2nd read re-runs
-    (DSB_TEST_FORCE_RERUN), deferred to the end of the batch and chunk by chunk; DSB_HEAVY_COST=1
-    sends every re-run read with a chain that way.  Records byte-identical to the production
+    (DSB_TEST_FORCE_RERUN), deferred to the end of the batch and chunk by chunk;
+    DSB_RETRY_HEAVY_COST=1 (the default) sends every re-run read with a chain that way.  Records byte-identical to the production
     library's run; the text path against the hermetic goldens with capacities below the defaults."""
     fq = tmp_path / "ont_x2.fq"
     fq.write_bytes(golden("ont.fq") * 2)
     carry = 1 << 20
     want, _ = run_worker(tmp_path, "prod", fixture_index, [fq], {}, lib=PROD_LIB, mode="batch", max_read_l=carry)
     for defer in ("1", "0"):
-        env = {"DSB_TEST_FORCE_RERUN": "2", "DSB_DEFER_RETRY": defer, "DSB_RETRY_SPEC": "1", "DSB_HEAVY_COST": cost,
+        env = {"DSB_TEST_FORCE_RERUN": "2", "DSB_DEFER_RETRY": defer, "DSB_RETRY_SPEC": "1", "DSB_RETRY_HEAVY_COST": cost,
                "DSB_HOST_TIMING": "1"}
         got, s = run_worker(tmp_path, f"rspec{defer}_{cost}", fixture_index, [fq], env, mode="batch", max_read_l=carry)
         assert s["calls"][0]["n_retry"] >= 2000, s["calls"][0]
@@ -177,7 +177,7 @@ def test_rerun_heavy_reads_scored_over_waves_byte_identical(fixture_index, tmp_p
         assert got[0] == want[0], (defer, cost)
     names = ("mixed", "ont", "ont_long")
     outs, summ = run_worker(tmp_path, f"rspec_scale0_{cost}", fixture_index, _golden_files(tmp_path, names),
-                            {"DSB_TEST_SCALE0": "1", "DSB_RETRY_SPEC": "1", "DSB_HEAVY_COST": cost})
+                            {"DSB_TEST_SCALE0": "1", "DSB_RETRY_SPEC": "1", "DSB_RETRY_HEAVY_COST": cost})
     assert sum(c["n_retry"] for c in summ["calls"]) > 0
     for name, out in zip(names, outs):
         assert out == golden(name + ".herm.sam"), (name, cost)
